@@ -1,0 +1,67 @@
+"""ctypes binding of ``liblcdb_gpu_snappy.so`` (C ABI: include/lcdb_gpu_snappy.h).
+
+There is no fallback: if the library is missing or fails to load, importing
+the codec raises.  The library is loaded from the package directory only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .build import LIB
+
+LGS_OK = 0
+LGS_ST_CORRUPT, LGS_ST_OK, LGS_ST_NOSPACE = 0, 1, 2
+LGS_MAX_BATCH_BLOCK = 65536
+
+_u8p = C.POINTER(C.c_uint8)
+_vp = C.c_void_p
+
+_SIGS = {
+    "ldb_snappy_encode_size": (C.c_int, [C.POINTER(C.c_size_t), C.c_size_t]),
+    "ldb_snappy_encode": (C.c_size_t, [_vp, _vp, C.c_size_t]),
+    "ldb_snappy_decode_size": (C.c_int, [C.POINTER(C.c_size_t), _vp, C.c_size_t]),
+    "ldb_snappy_decode": (C.c_int, [_vp, _vp, C.c_size_t]),
+    "lgs_encode_bound": (C.c_size_t, [C.c_size_t]),
+    "lgs_encode_batch_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
+    "lgs_decode_batch_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32,
+                                       C.c_uint32, _vp]),
+    "lgs_encode_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32]),
+    "lgs_decode_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32]),
+    "lgs_device_count": (C.c_int, []),
+    "lgs_set_device": (C.c_int, [C.c_int]),
+    "lgs_last_error": (C.c_char_p, []),
+    "lgs_version": (C.c_char_p, []),
+}
+
+# Every symbol include/lcdb_gpu_snappy.h declares.
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load (once) and return the native library; raises if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise ImportError(
+                f"lcdb_amd native library not built: {LIB} is missing "
+                "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        handle = C.CDLL(LIB, mode=C.RTLD_LOCAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+class LgsError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != LGS_OK:
+        msg = lib().lgs_last_error().decode(errors="replace")
+        raise LgsError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,82 @@
+"""Build the native pieces in-tree (gfx950 only).
+
+* ``lcdb_amd/liblcdb_gpu_snappy.so`` -- HIP kernels + C ABI (hipcc,
+  ``--offload-arch=gfx950``), declared in ``include/lcdb_gpu_snappy.h``.
+* ``lcdb_amd/libcorpus.so`` -- host C generator of db_bench-shaped blocks.
+* ``oracle/`` -- the parity checker (``make -C oracle``); test infrastructure
+  only, built here so the GPU box receives it prebuilt.
+
+The built ``.so`` files are git-ignored but travel to the GPU box with the
+repo snapshot; nothing is JIT-compiled at import time.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "lcdb_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "liblcdb_gpu_snappy.so")
+CORPUS_LIB = os.path.join(PKG, "libcorpus.so")
+
+HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip"]
+HIP_HEADERS = ["lgs_device.h", "lgs_launch.h"]
+ARCH = "gfx950"
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build lcdb_amd)")
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    print("+", " ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+
+
+def build_hip(force: bool = False, extra: list[str] | None = None) -> str:
+    srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
+    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [
+        os.path.join(ROOT, "include", "lcdb_gpu_snappy.h")]
+    if force or _stale(LIB, deps):
+        tmp = LIB + ".tmp"
+        _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
+              "-Wall", "-Wextra", *srcs, "-o", tmp, *(extra or [])])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_corpus(force: bool = False) -> str:
+    src = os.path.join(CSRC, "corpus.c")
+    if force or _stale(CORPUS_LIB, [src]):
+        tmp = CORPUS_LIB + ".tmp"
+        _run(["gcc", "-std=gnu99", "-O2", "-Wall", "-Wextra", "-fPIC", "-shared", src,
+              "-o", tmp])
+        os.replace(tmp, CORPUS_LIB)
+    return CORPUS_LIB
+
+
+def build_oracle() -> None:
+    _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+def build_all(force: bool = False) -> None:
+    build_corpus(force)
+    build_oracle()
+    build_hip(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

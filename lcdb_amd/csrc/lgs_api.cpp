@@ -1,0 +1,477 @@
+// lgs_api.cpp -- host runtime and C ABI of the gfx950 Snappy codec
+// (declarations, and the reference interfaces they replace:
+// include/lcdb_gpu_snappy.h).
+//
+// Per calling thread: one non-blocking HIP stream on the selected device, a
+// growable device arena and a growable pinned host arena.  lcdb enters the
+// codec concurrently from user threads (reads) and its compaction thread
+// (writes) (db_impl.c:1614-1652), so nothing here is shared between threads
+// except the HIP runtime itself.
+//
+// No compression or decompression happens on the host.  The host only moves
+// bytes (pageable <-> pinned <-> device), computes the size bound
+// (snappy.c:347-362) and reads the varint32 size header (snappy.c:386-399).
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/lcdb_gpu_snappy.h"
+
+#include "lgs_launch.h"
+
+namespace lgs {
+namespace {
+
+constexpr uint32_t kChunk = 65536;   // snappy.c:28
+
+thread_local char t_err[512];
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(t_err, sizeof t_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define LGS_HIP(call)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (call);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return fail(LGS_EHIP, "%s failed: %s", #call, hipGetErrorString(e_));        \
+  } while (0)
+
+#define LGS_TRY(expr)              \
+  do {                             \
+    int r_ = (expr);               \
+    if (r_ != LGS_OK) return r_;   \
+  } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) & ~(a - 1); }
+
+size_t bound_of(size_t n) { return 32 + n + n / 6; }   // snappy.c:354
+
+struct Ctx {
+  int device = -1;          // device this context's resources live on
+  int want_device = -1;     // lgs_set_device() choice (-1: current device)
+  hipStream_t stream = nullptr;
+  uint8_t* d_buf = nullptr;
+  size_t d_cap = 0;
+  uint8_t* h_buf = nullptr; // pinned
+  size_t h_cap = 0;
+};
+
+// Deliberately never destroyed: freeing HIP resources from thread-exit
+// destructors can run after the runtime is torn down at process exit.
+thread_local Ctx t_ctx;
+
+int ctx_ready(Ctx& c) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(LGS_ENODEV, "no HIP device visible");
+  int dev = c.want_device;
+  if (dev < 0) {
+    LGS_HIP(hipGetDevice(&dev));
+  } else {
+    if (dev >= count) return fail(LGS_ENODEV, "device %d not present (%d visible)", dev, count);
+    LGS_HIP(hipSetDevice(dev));
+  }
+  if (c.device != dev || c.stream == nullptr) {
+    // A thread that switches devices abandons the previous device's buffers
+    // (they are not freed from the wrong device).
+    const int keep = c.want_device;
+    c = Ctx{};
+    c.want_device = keep;
+    c.device = dev;
+    LGS_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  }
+  return LGS_OK;
+}
+
+int ctx_reserve(Ctx& c, size_t dev_bytes, size_t pin_bytes) {
+  if (dev_bytes > c.d_cap) {
+    if (c.d_buf) LGS_HIP(hipFree(c.d_buf));
+    c.d_buf = nullptr;
+    c.d_cap = 0;
+    const size_t cap = align_up(dev_bytes + dev_bytes / 4, 1 << 20);
+    if (hipMalloc(&c.d_buf, cap) != hipSuccess) return fail(LGS_ENOMEM, "hipMalloc(%zu) failed", cap);
+    c.d_cap = cap;
+  }
+  if (pin_bytes > c.h_cap) {
+    if (c.h_buf) LGS_HIP(hipHostFree(c.h_buf));
+    c.h_buf = nullptr;
+    c.h_cap = 0;
+    const size_t cap = align_up(pin_bytes + pin_bytes / 4, 1 << 20);
+    if (hipHostMalloc(&c.h_buf, cap, hipHostMallocDefault) != hipSuccess)
+      return fail(LGS_ENOMEM, "hipHostMalloc(%zu) failed", cap);
+    c.h_cap = cap;
+  }
+  return LGS_OK;
+}
+
+// Offsets into a staging area, 256-byte aligned.  The pinned arena and the
+// device arena use the same layout, so an upload or a download is a single
+// contiguous hipMemcpyAsync.
+struct Layout {
+  size_t at = 0;
+  size_t take(size_t bytes) {
+    const size_t o = at;
+    at = align_up(at + bytes, 256);
+    return o;
+  }
+};
+
+// coding.h:169-204 on the host, for the size header only.
+int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
+  uint32_t acc = 0;
+  unsigned sh = 0;
+  for (size_t i = 0; sh <= 28 && i < n; sh += 7, ++i) {
+    const uint32_t b = p[i];
+    if ((b & 0x80u) == 0) {
+      *v = acc | (b << sh);
+      return 1;
+    }
+    acc |= (b & 0x7fu) << sh;
+  }
+  *v = 0;
+  return 0;
+}
+
+[[noreturn]] void die(const char* what) {
+  fprintf(stderr, "lcdb_gpu_snappy: %s failed: %s\n", what, t_err);
+  abort();
+}
+
+// Encode one host block of any length on the GPU.
+int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  if (xn > 0x7fffffffu) return fail(LGS_EINVAL, "input of %zu bytes too large", xn);
+  const uint32_t n = (uint32_t)xn;
+  // snappy.c:370-381: full 64 KiB chunks, then the remainder (if any).
+  const uint32_t nit = n <= kChunk ? 1u : (n + kChunk - 1) / kChunk;
+  const bool single = nit == 1;
+
+  size_t scratch_bytes = 0;
+  for (uint32_t j = 0; j < nit; ++j) {
+    const uint32_t len = j + 1 < nit ? kChunk : n - j * kChunk;
+    scratch_bytes += align_up(bound_of(len) + 8, 16);
+  }
+  const size_t final_bytes = bound_of(n);
+
+  Layout L;  // upload | download | device-only
+  const size_t o_in = L.take(n + 16);
+  const size_t o_ioff = L.take(8 * (size_t)nit);
+  const size_t o_ilen = L.take(4 * (size_t)nit);
+  const size_t o_ooff = L.take(8 * (size_t)nit);
+  const size_t o_hdr = L.take(4 * (size_t)nit);
+  const size_t up_end = L.at;
+  const size_t o_olen = L.take(4 * (size_t)nit);
+  const size_t o_dst_off = L.take(8 * (size_t)nit);
+  const size_t o_final = L.take(final_bytes + 16);
+  const size_t down_end = L.at;
+  const size_t o_scratch = L.take(single ? 0 : scratch_bytes);
+  LGS_TRY(ctx_reserve(c, L.at, down_end));
+
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  memcpy(h + o_in, xp, n);
+  uint64_t* ioff = (uint64_t*)(h + o_ioff);
+  uint32_t* ilen = (uint32_t*)(h + o_ilen);
+  uint64_t* ooff = (uint64_t*)(h + o_ooff);
+  uint32_t* hdr = (uint32_t*)(h + o_hdr);
+  size_t sat = 0;
+  for (uint32_t j = 0; j < nit; ++j) {
+    const uint32_t len = j + 1 < nit ? kChunk : n - j * kChunk;
+    ioff[j] = o_in + (size_t)j * kChunk;
+    ilen[j] = len;
+    hdr[j] = j == 0 ? n : 0xffffffffu;
+    ooff[j] = single ? o_final : o_scratch + sat;
+    sat += align_up(bound_of(len) + 8, 16);
+  }
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+
+  EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
+               (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen),
+               (const uint32_t*)(d + o_hdr), nullptr, nit};
+  LGS_HIP(launch_encode(a, single ? n : kChunk, c.stream));
+
+  uint32_t* olen = (uint32_t*)(h + o_olen);
+  size_t total = 0;
+  if (single) {
+    LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, down_end - o_olen, hipMemcpyDeviceToHost,
+                           c.stream));
+    LGS_HIP(hipStreamSynchronize(c.stream));
+    total = olen[0];
+  } else {
+    // Chunk outputs are concatenated on the device once their lengths are
+    // known (one small round trip for the lengths).
+    LGS_HIP(hipMemcpyAsync(olen, d + o_olen, 4 * (size_t)nit, hipMemcpyDeviceToHost, c.stream));
+    LGS_HIP(hipStreamSynchronize(c.stream));
+    uint64_t* doff = (uint64_t*)(h + o_dst_off);
+    for (uint32_t j = 0; j < nit; ++j) {
+      doff[j] = o_final + total;
+      total += olen[j];
+    }
+    LGS_HIP(hipMemcpyAsync(d + o_dst_off, doff, 8 * (size_t)nit, hipMemcpyHostToDevice, c.stream));
+    LGS_HIP(launch_concat(d, (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_olen), d,
+                          (const uint64_t*)(d + o_dst_off), nit, c.stream));
+    LGS_HIP(hipMemcpyAsync(h + o_final, d + o_final, total, hipMemcpyDeviceToHost, c.stream));
+    LGS_HIP(hipStreamSynchronize(c.stream));
+  }
+  if (total > final_bytes) return fail(LGS_EHIP, "encoded length %zu exceeds bound", total);
+  memcpy(zp, h + o_final, total);
+  *written = total;
+  return LGS_OK;
+}
+
+// Decode one host block on the GPU.  *ok = reference decode result.
+int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
+  uint32_t want = 0;
+  if (!read_varint32(&want, xp, xn) || want > 0x7fffffffu) {  // snappy.c:405-409
+    *ok = 0;
+    return LGS_OK;
+  }
+  if (xn > 0xffffffffu) return fail(LGS_EINVAL, "input of %zu bytes too large", xn);
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  const uint32_t n = (uint32_t)xn;
+
+  Layout L;
+  const size_t o_in = L.take(n + 16);
+  const size_t o_ioff = L.take(8);
+  const size_t o_ilen = L.take(4);
+  const size_t o_ooff = L.take(8);
+  const size_t o_ocap = L.take(4);
+  const size_t up_end = L.at;
+  const size_t o_st = L.take(4);
+  const size_t o_olen = L.take(4);
+  const size_t o_out = L.take((size_t)want + 16);
+  const size_t down_end = L.at;
+  LGS_TRY(ctx_reserve(c, down_end, down_end));
+
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  memcpy(h + o_in, xp, n);
+  *(uint64_t*)(h + o_ioff) = o_in;
+  *(uint32_t*)(h + o_ilen) = n;
+  *(uint64_t*)(h + o_ooff) = o_out;
+  *(uint32_t*)(h + o_ocap) = want;
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
+               (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
+               (uint32_t*)(d + o_olen), d + o_st, nullptr, 1};
+  LGS_HIP(launch_decode(a, want, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint8_t st = h[o_st];
+  if (st == LGS_ST_OK) memcpy(zp, h + o_out, want);
+  *ok = st == LGS_ST_OK;
+  return LGS_OK;
+}
+
+}  // namespace
+}  // namespace lgs
+
+using namespace lgs;
+
+extern "C" {
+
+// ---- drop-in (src/util/snappy.h:28-38) ----
+
+int ldb_snappy_encode_size(size_t* zn, size_t xn) {   // snappy.c:347-362
+  if (xn > 0x7fffffff) return 0;
+  const size_t n = bound_of(xn);
+  if (n > 0x7fffffff) return 0;
+  *zn = n;
+  return 1;
+}
+
+size_t ldb_snappy_encode(uint8_t* zp, const uint8_t* xp, size_t xn) {
+  size_t written = 0;
+  if (encode_one(zp, xp, xn, &written) != LGS_OK) die("ldb_snappy_encode");
+  return written;
+}
+
+int ldb_snappy_decode_size(size_t* zn, const uint8_t* xp, size_t xn) {   // snappy.c:386-399
+  uint32_t v;
+  if (!read_varint32(&v, xp, xn)) return 0;
+  if (v > 0x7fffffffu) return 0;
+  *zn = v;
+  return 1;
+}
+
+int ldb_snappy_decode(uint8_t* zp, const uint8_t* xp, size_t xn) {
+  int ok = 0;
+  if (decode_one(zp, xp, xn, &ok) != LGS_OK) die("ldb_snappy_decode");
+  return ok;
+}
+
+// ---- batched API ----
+
+size_t lgs_encode_bound(size_t n) { return bound_of(n); }
+
+int lgs_encode_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                         uint8_t* d_out, const uint64_t* d_out_off, uint32_t* d_out_len,
+                         uint32_t n, uint32_t max_in_len, void* stream) {
+  if (n == 0) return LGS_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len)
+    return fail(LGS_EINVAL, "NULL argument");
+  if (max_in_len > LGS_MAX_BATCH_BLOCK)
+    return fail(LGS_EINVAL, "max_in_len %u > %u", max_in_len, LGS_MAX_BATCH_BLOCK);
+  EncodeArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nullptr, nullptr, n};
+  LGS_HIP(launch_encode(a, max_in_len, (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_decode_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                         uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                         uint32_t* d_out_len, uint8_t* d_status, uint32_t n,
+                         uint32_t max_out_cap, void* stream) {
+  if (n == 0) return LGS_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len ||
+      !d_status)
+    return fail(LGS_EINVAL, "NULL argument");
+  DecodeArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+               nullptr, n};
+  LGS_HIP(launch_decode(a, max_out_cap, (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                          uint8_t* out, const uint64_t* out_off, uint32_t* out_len, uint32_t n) {
+  if (n == 0) return LGS_OK;
+  if (!in || !in_off || !in_len || !out || !out_off || !out_len)
+    return fail(LGS_EINVAL, "NULL argument");
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  size_t in_total = 0, out_total = 0;
+  uint32_t max_in = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (in_len[i] > LGS_MAX_BATCH_BLOCK)
+      return fail(LGS_EINVAL, "block %u: %u bytes > %u", i, in_len[i], LGS_MAX_BATCH_BLOCK);
+    in_total += align_up(in_len[i], 16);
+    out_total += align_up(bound_of(in_len[i]), 16);
+    if (in_len[i] > max_in) max_in = in_len[i];
+  }
+  Layout L;
+  const size_t o_in = L.take(in_total + 16);
+  const size_t o_ioff = L.take(8 * (size_t)n);
+  const size_t o_ilen = L.take(4 * (size_t)n);
+  const size_t o_ooff = L.take(8 * (size_t)n);
+  const size_t up_end = L.at;
+  const size_t o_olen = L.take(4 * (size_t)n);
+  const size_t o_out = L.take(out_total + 16);
+  const size_t down_end = L.at;
+  LGS_TRY(ctx_reserve(c, down_end, down_end));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* ioff = (uint64_t*)(h + o_ioff);
+  uint32_t* ilen = (uint32_t*)(h + o_ilen);
+  uint64_t* ooff = (uint64_t*)(h + o_ooff);
+  size_t ia = o_in, oa = o_out;
+  for (uint32_t i = 0; i < n; ++i) {
+    memcpy(h + ia, in + in_off[i], in_len[i]);
+    ioff[i] = ia;
+    ilen[i] = in_len[i];
+    ooff[i] = oa;
+    ia += align_up(in_len[i], 16);
+    oa += align_up(bound_of(in_len[i]), 16);
+  }
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
+               (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen), nullptr, nullptr, n};
+  LGS_HIP(launch_encode(a, max_in, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, down_end - o_olen, hipMemcpyDeviceToHost,
+                         c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint32_t* olen = (const uint32_t*)(h + o_olen);
+  for (uint32_t i = 0; i < n; ++i) {
+    memcpy(out + out_off[i], h + ooff[i], olen[i]);
+    out_len[i] = olen[i];
+  }
+  return LGS_OK;
+}
+
+int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                          uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                          uint32_t* out_len, uint8_t* status, uint32_t n) {
+  if (n == 0) return LGS_OK;
+  if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !status)
+    return fail(LGS_EINVAL, "NULL argument");
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  size_t in_total = 0, out_total = 0;
+  uint32_t max_cap = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    in_total += align_up(in_len[i], 16);
+    out_total += align_up(out_cap[i], 16);
+    if (out_cap[i] > max_cap) max_cap = out_cap[i];
+  }
+  Layout L;
+  const size_t o_in = L.take(in_total + 16);
+  const size_t o_ioff = L.take(8 * (size_t)n);
+  const size_t o_ilen = L.take(4 * (size_t)n);
+  const size_t o_ooff = L.take(8 * (size_t)n);
+  const size_t o_ocap = L.take(4 * (size_t)n);
+  const size_t up_end = L.at;
+  const size_t o_st = L.take((size_t)n);
+  const size_t o_olen = L.take(4 * (size_t)n);
+  const size_t o_out = L.take(out_total + 16);
+  const size_t down_end = L.at;
+  LGS_TRY(ctx_reserve(c, down_end, down_end));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* ioff = (uint64_t*)(h + o_ioff);
+  uint32_t* ilen = (uint32_t*)(h + o_ilen);
+  uint64_t* ooff = (uint64_t*)(h + o_ooff);
+  uint32_t* ocap = (uint32_t*)(h + o_ocap);
+  size_t ia = o_in, oa = o_out;
+  for (uint32_t i = 0; i < n; ++i) {
+    memcpy(h + ia, in + in_off[i], in_len[i]);
+    ioff[i] = ia;
+    ilen[i] = in_len[i];
+    ooff[i] = oa;
+    ocap[i] = out_cap[i];
+    ia += align_up(in_len[i], 16);
+    oa += align_up(out_cap[i], 16);
+  }
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
+               (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
+               (uint32_t*)(d + o_olen), d + o_st, nullptr, n};
+  LGS_HIP(launch_decode(a, max_cap, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint32_t* olen = (const uint32_t*)(h + o_olen);
+  for (uint32_t i = 0; i < n; ++i) {
+    status[i] = h[o_st + i];
+    out_len[i] = olen[i];
+    if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
+  }
+  return LGS_OK;
+}
+
+int lgs_device_count(void) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess) return 0;
+  return count;
+}
+
+int lgs_set_device(int device) {
+  int count = lgs_device_count();
+  if (device < 0 || device >= count)
+    return fail(LGS_ENODEV, "device %d not present (%d visible)", device, count);
+  t_ctx.want_device = device;
+  return LGS_OK;
+}
+
+const char* lgs_last_error(void) { return t_err; }
+
+const char* lgs_version(void) { return "lcdb_gpu_snappy 0.1 gfx950"; }
+
+}  // extern "C"

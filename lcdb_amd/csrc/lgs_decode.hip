@@ -1,0 +1,317 @@
+// lgs_decode.hip -- batched Snappy block decoder for gfx950 (MI355X).
+//
+// Semantics: lcdb src/util/snappy.c:386-412 (snappy_decode_size/decode) and
+// decode_blocks (snappy.c:201-341), restated for a wave64:
+//   * one wave owns one block; WAVES independent waves per workgroup;
+//   * the compressed block is staged global->LDS with 16-byte lanes, the
+//     decoded block is built in LDS and streamed out with 16-byte stores;
+//   * the tag walk is a scalar (SGPR) loop: each tag is read as one 8-byte
+//     LDS window, decoded on the SALU, and its bytes are moved by the lanes;
+//   * every reject condition of the reference is checked in the same order,
+//     so the per-block accept/reject bit equals the reference's.
+// Blocks whose compressed length exceeds the class's LDS staging area are
+// decoded from global memory by the same loop (still on the GPU).
+//
+// status[i]: 1 = ok, 0 = corrupt (reference returns 0), 2 = decoded length
+// exceeds out_cap[i] (batch-API capacity check; the drop-in sizes the output
+// from the header so it never sees 2).
+#include "lgs_device.h"
+#include "lgs_launch.h"
+
+namespace lgs {
+
+// Byte source over an LDS-staged stream (byte k at base[k]).
+struct LdsStream {
+  const uint8_t* base;
+  __device__ uint64_t win(uint32_t pos) const { return uni64(lds_ld64(base, pos)); }
+  __device__ uint8_t byte(uint32_t pos) const { return base[pos]; }
+};
+
+// Byte source over the stream in global memory (oversized blocks only).
+// Window bytes at or past `len` read as zero and are never consumed.
+struct GlobalStream {
+  const uint8_t* base;
+  uint32_t len;
+  __device__ uint64_t win(uint32_t pos) const {
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < 8; ++i)
+      if (pos + i < len) v |= (uint64_t)base[pos + i] << (8 * i);
+    return uni64(v);
+  }
+  __device__ uint8_t byte(uint32_t pos) const { return base[pos]; }
+};
+
+// Decode one stream into `o` (LDS).  Returns 1 ok / 0 corrupt / 2 too big.
+template <class Src>
+__device__ uint32_t decode_stream(const Src& src, uint32_t slen, uint8_t* o,
+                                  uint32_t cap, uint32_t* want_out) {
+  const uint32_t lane = lane_id();
+
+  // varint32 header, coding.h:169-204 (<= 5 bytes, continuation on the
+  // fifth byte or running out of input is a failure).
+  uint64_t w = src.win(0);
+  uint32_t want = 0, pos = 0;
+  bool hdr_ok = false;
+  for (uint32_t i = 0; i < 5 && i < slen; ++i) {
+    uint32_t b = (uint32_t)(w >> (8 * i)) & 0xffu;
+    if ((b & 0x80u) == 0) {
+      want |= b << (7 * i);
+      pos = i + 1;
+      hdr_ok = true;
+      break;
+    }
+    want |= (b & 0x7fu) << (7 * i);
+  }
+  if (!hdr_ok || want > 0x7fffffffu) return 0;   // snappy.c:405-409
+  if (want > cap) return 2;
+  *want_out = want;
+
+  uint32_t left = slen - pos;
+  uint32_t made = 0;
+
+  while (left > 0) {                                // snappy.c:208
+    const uint64_t t = src.win(pos);
+    const uint32_t tag = (uint32_t)t & 0xffu;
+    const uint32_t kind = tag & 3u;
+
+    if (kind == 0) {                                // literal, snappy.c:210-273
+      uint32_t m = tag >> 2;
+      uint32_t hl = 1;
+      if (m >= 60) {
+        const uint32_t extra = m - 59;              // 1..4 length bytes
+        if (left - 1 < extra) return 0;
+        const uint32_t hi = (uint32_t)(t >> 8);
+        m = extra == 4 ? hi : (hi & ((1u << (8 * extra)) - 1u));
+        hl += extra;
+      }
+      if (m >= 0x7fffffffu) return 0;               // snappy.c:258
+      const uint32_t len = m + 1;
+      pos += hl;
+      left -= hl;
+      if (len > want - made || len > left) return 0;  // snappy.c:263
+      for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
+        const uint32_t j = j0 + lane;
+        if (j < len) o[made + j] = src.byte(pos + j);
+      }
+      order();
+      made += len;
+      pos += len;
+      left -= len;
+      continue;
+    }
+
+    uint32_t len, dist, hl;
+    if (kind == 1) {                                // COPY1, snappy.c:276-287
+      if (left < 2) return 0;
+      len = 4 + ((tag >> 2) & 7u);
+      dist = ((tag & 0xe0u) << 3) | ((uint32_t)(t >> 8) & 0xffu);
+      hl = 2;
+    } else if (kind == 2) {                         // COPY2, snappy.c:289-301
+      if (left < 3) return 0;
+      len = 1 + (tag >> 2);
+      dist = (uint32_t)(t >> 8) & 0xffffu;
+      hl = 3;
+    } else {                                        // COPY4, snappy.c:303-317
+      if (left < 5) return 0;
+      len = 1 + (tag >> 2);
+      dist = (uint32_t)(t >> 8);
+      hl = 5;
+    }
+    pos += hl;
+    left -= hl;
+    if (dist == 0 || dist >= 0x80000000u) return 0;   // snappy.c:320
+    if (made < dist || len > want - made) return 0;   // snappy.c:323
+
+    // len <= 64: one lane per output byte.  An overlapping copy (dist <
+    // len) repeats the dist-byte pattern, which is what the reference's
+    // forward byte loop (snappy.c:329-330) produces.
+    if (lane < len) {
+      const uint32_t from = made - dist + (dist >= len ? lane : lane % dist);
+      const uint8_t v = o[from];
+      o[made + lane] = v;
+    }
+    order();
+    made += len;
+  }
+
+  return made == want ? 1u : 0u;                    // snappy.c:337
+}
+
+// Stream the decoded bytes o[shift .. shift+len) (LDS) to dst, where
+// shift == dst & 15: every full granule is one 16-byte store.
+__device__ __forceinline__ void flush_out(uint8_t* dst, const uint8_t* o, uint32_t len) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
+  const uint32_t shift = (uint32_t)(a & 15u);
+  uint8_t* g = reinterpret_cast<uint8_t*>(a - shift);
+  const uint32_t end = shift + len;
+  const uint32_t n16 = (end + 15u) >> 4;
+  for (uint32_t c = lane_id(); c < n16; c += kWave) {
+    const uint32_t lo = c << 4, hi = lo + 16;
+    if (lo >= shift && hi <= end) {
+      *reinterpret_cast<uint4*>(g + lo) = *reinterpret_cast<const uint4*>(o + lo);
+    } else {
+      for (uint32_t b = lo; b < hi; ++b)
+        if (b >= shift && b < end) g[b] = o[b];
+    }
+  }
+}
+
+template <uint32_t OUT_CAP, uint32_t IN_CAP, uint32_t WAVES>
+__global__ __launch_bounds__(64 * WAVES) void decode_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][OUT_CAP + 32];
+
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t slot = blockIdx.x * WAVES + wv;
+  if (slot >= n) return;
+  const uint32_t i = index ? index[slot] : slot;
+
+  const uint8_t* src = in + in_off[i];
+  const uint32_t slen = in_len[i];
+  uint8_t* dst = out + out_off[i];
+  const uint32_t cap = out_cap[i] < OUT_CAP ? out_cap[i] : OUT_CAP;
+  const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+  uint8_t* o = &s_out[wv][oshift];
+
+  uint32_t want = 0, st;
+  if (slen <= IN_CAP) {
+    const uint32_t sh = stage_in(&s_in[wv][0], src, slen);
+    order();
+    st = decode_stream(LdsStream{&s_in[wv][sh]}, slen, o, cap, &want);
+  } else {
+    st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
+  }
+  if (st == 1) flush_out(dst, o, want);
+  if (lane_id() == 0) {
+    status[i] = (uint8_t)st;
+    out_len[i] = st == 1 ? want : 0;
+  }
+}
+
+// Outputs larger than every LDS class: the same tag loop writing straight to
+// global memory.  A copy reads bytes this wave stored earlier, so every store
+// is drained (vmcnt) and the reads bypass L1 (agent-scope loads).
+__device__ __forceinline__ uint8_t gl_byte(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint8_t)(v >> (8 * (a & 3u)));
+}
+
+__global__ __launch_bounds__(64) void decode_big_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n) {
+  const uint32_t slot = blockIdx.x;
+  if (slot >= n) return;
+  const uint32_t i = index ? index[slot] : slot;
+  const uint32_t lane = lane_id();
+  const GlobalStream src{in + in_off[i], in_len[i]};
+  const uint32_t slen = in_len[i];
+  uint8_t* o = out + out_off[i];
+  const uint32_t cap = out_cap[i];
+
+  uint32_t st = 0, want = 0;
+  do {
+    uint64_t w = src.win(0);
+    uint32_t pos = 0;
+    bool hdr_ok = false;
+    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
+      uint32_t b = (uint32_t)(w >> (8 * k)) & 0xffu;
+      if ((b & 0x80u) == 0) { want |= b << (7 * k); pos = k + 1; hdr_ok = true; break; }
+      want |= (b & 0x7fu) << (7 * k);
+    }
+    if (!hdr_ok || want > 0x7fffffffu) { st = 0; break; }
+    if (want > cap) { st = 2; break; }
+    uint32_t left = slen - pos, made = 0;
+    st = 1;
+    while (left > 0) {
+      const uint64_t t = src.win(pos);
+      const uint32_t tag = (uint32_t)t & 0xffu, kind = tag & 3u;
+      if (kind == 0) {
+        uint32_t m = tag >> 2, hl = 1;
+        if (m >= 60) {
+          const uint32_t extra = m - 59;
+          if (left - 1 < extra) { st = 0; break; }
+          const uint32_t hi = (uint32_t)(t >> 8);
+          m = extra == 4 ? hi : (hi & ((1u << (8 * extra)) - 1u));
+          hl += extra;
+        }
+        if (m >= 0x7fffffffu) { st = 0; break; }
+        const uint32_t len = m + 1;
+        pos += hl; left -= hl;
+        if (len > want - made || len > left) { st = 0; break; }
+        for (uint32_t j = lane; j < len; j += kWave) o[made + j] = src.byte(pos + j);
+        made += len; pos += len; left -= len;
+        continue;
+      }
+      uint32_t len, dist, hl;
+      if (kind == 1) {
+        if (left < 2) { st = 0; break; }
+        len = 4 + ((tag >> 2) & 7u); dist = ((tag & 0xe0u) << 3) | ((uint32_t)(t >> 8) & 0xffu); hl = 2;
+      } else if (kind == 2) {
+        if (left < 3) { st = 0; break; }
+        len = 1 + (tag >> 2); dist = (uint32_t)(t >> 8) & 0xffffu; hl = 3;
+      } else {
+        if (left < 5) { st = 0; break; }
+        len = 1 + (tag >> 2); dist = (uint32_t)(t >> 8); hl = 5;
+      }
+      pos += hl; left -= hl;
+      if (dist == 0 || dist >= 0x80000000u) { st = 0; break; }
+      if (made < dist || len > want - made) { st = 0; break; }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane < len) {
+        const uint32_t from = made - dist + (dist >= len ? lane : lane % dist);
+        o[made + lane] = gl_byte(o + from);
+      }
+      made += len;
+    }
+    if (st == 1 && made != want) st = 0;
+  } while (0);
+  if (lane == 0) {
+    status[i] = (uint8_t)st;
+    out_len[i] = st == 1 ? want : 0;
+  }
+}
+
+}  // namespace lgs
+
+// ---------------------------------------------------------------------------
+// Launchers (internal; the C ABI is in lgs_api.cpp).
+// Decode classes by the largest output a launch must hold in LDS.
+// ---------------------------------------------------------------------------
+namespace lgs {
+
+template <uint32_t OUT_CAP, uint32_t IN_CAP, uint32_t WAVES>
+static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
+  const uint32_t grid = (a.n + WAVES - 1) / WAVES;
+  hipLaunchKernelGGL((decode_kernel<OUT_CAP, IN_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
+                     a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
+                     a.index, a.n);
+  return hipGetLastError();
+}
+
+// Class limits (bytes of decoded output held in LDS per wave).
+constexpr uint32_t kDecCap0 = 4608;    // fillseq "4 KiB" blocks (max 4208 B)
+constexpr uint32_t kDecCap1 = 16896;   // 16 KiB class
+constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoot)
+
+hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 5632, 1>(a, s);
+  if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 19968, 1>(a, s);
+  if (max_out <= kDecCap2) return launch_decode_cls<kDecCap2, 76800, 1>(a, s);
+  hipLaunchKernelGGL(decode_big_kernel, dim3(a.n), dim3(64), 0, s, a.in, a.in_off, a.in_len,
+                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+  return hipGetLastError();
+}
+
+}  // namespace lgs

@@ -1,0 +1,94 @@
+// lgs_device.h -- device-side helpers shared by the gfx950 Snappy kernels.
+//
+// Format constants and arithmetic follow lcdb's src/util/snappy.c (file:line
+// cited per item).  Everything here is wave64 code: "uniform" values live in
+// SGPRs (v_readfirstlane) so control flow is scalar, and lane-parallel byte
+// work uses the 64 lanes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lgs {
+
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kTableCap = 2048;      // MAX_TABLE_SIZE, snappy.c:25
+constexpr uint32_t kMargin = 15;          // INPUT_MARGIN, snappy.c:26
+constexpr uint32_t kMinBlock = 17;        // MIN_BLOCK_SIZE, snappy.c:27
+constexpr uint32_t kChunk = 65536;        // MAX_BLOCK_SIZE, snappy.c:28
+constexpr uint32_t kHashMul = 0x1e35a7bdu;  // snappy.c:46
+
+// Probe schedule of the literal search (snappy.c:138-143): probe k sits at
+// start + kProbeOff[k]; skip starts at 32 and grows by skip >> 5 after each
+// probe.  The schedule depends only on k, so a wave can place 64 probes at
+// once.  384 entries cover a 64 KiB chunk (the offset passes 65536 near k=250).
+constexpr int kProbeTab = 384;
+struct ProbeTable {
+  uint32_t off[kProbeTab + 1];
+  constexpr ProbeTable() : off() {
+    uint32_t skip = 32, at = 0;
+    for (int k = 0; k <= kProbeTab; ++k) {
+      off[k] = at;
+      at += skip >> 5;
+      skip += skip >> 5;
+    }
+  }
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// snappy.c:44-47 (argument truncated to 32 bits at every call site).
+__device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) {
+  return (v * kHashMul) >> shift;
+}
+
+// Compiler-only barrier: LDS accesses of one wave execute in issue order in
+// hardware; this stops hipcc from reordering a lane's LDS load above another
+// lane's earlier LDS store that it cannot see it depends on.
+__device__ __forceinline__ void order() { asm volatile("" ::: "memory"); }
+
+// Unaligned little-endian 32-bit load from a 4-byte-aligned LDS base: two
+// aligned dwords + v_alignbyte (coding.h:33-40 semantics).
+__device__ __forceinline__ uint32_t lds_ld32(const uint8_t* base, uint32_t at) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], at & 3u);
+}
+
+// 8 bytes starting at `at` (bytes at..at+7).
+__device__ __forceinline__ uint64_t lds_ld64(const uint8_t* base, uint32_t at) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));
+  uint32_t a = w[0], b = w[1], c = w[2];
+  uint32_t s = at & 3u;
+  uint32_t lo = __builtin_amdgcn_alignbyte(b, a, s);
+  uint32_t hi = __builtin_amdgcn_alignbyte(c, b, s);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Copy `len` bytes global->LDS: the LDS image keeps the source's alignment
+// mod 16 (byte k of the source lands at lds[(src & 15) + k]) so that every
+// lane moves one aligned 16-byte granule.  Returns the LDS shift (src & 15).
+// Reads may touch the aligned 16-byte granules that contain the first and
+// last byte, never a different page.
+__device__ __forceinline__ uint32_t stage_in(uint8_t* lds, const uint8_t* src, uint32_t len) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+  const uint32_t shift = (uint32_t)(a & 15u);
+  const uint4* g = reinterpret_cast<const uint4*>(a - shift);
+  uint4* l = reinterpret_cast<uint4*>(lds);
+  const uint32_t n16 = (shift + len + 15u) >> 4;
+  for (uint32_t c = lane_id(); c < n16; c += kWave) l[c] = g[c];
+  // Zero pad one granule past the end so fixed-width window reads are defined.
+  if (lane_id() == 0) l[n16] = make_uint4(0, 0, 0, 0);
+  return shift;
+}
+
+}  // namespace lgs

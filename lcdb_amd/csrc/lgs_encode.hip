@@ -1,0 +1,291 @@
+// lgs_encode.hip -- batched Snappy block encoder for gfx950 (MI355X),
+// byte-identical to lcdb's src/util/snappy.c:104-195 (encode_block) and
+// snappy.c:364-384 (snappy_encode).
+//
+// One wave owns one work item (a whole block <= 64 KiB, or one 64 KiB chunk
+// of a larger block).  The input is staged in LDS with the 2048-entry u16
+// hash table (snappy.c:25,107).  The greedy parse is serial by definition;
+// the wave makes it cheap instead of parallel-but-different:
+//
+//  * literal search: the probe positions of snappy.c:138-143 depend only on
+//    the probe's index k since the search started (skip = 32, += skip >> 5),
+//    so 64 lanes take probes k..k+63 at once.  Each lane hashes its position
+//    and reads its candidate from the table as it stood before the batch.
+//    That is exact for every lane whose hash no earlier lane of the batch
+//    shares; a lane-id scatter/gather through LDS finds the first lane that
+//    collides and the batch is cut there (lanes before it are all exact,
+//    lane 0 always is).  The first lane whose 4-byte compare matches ends the
+//    search; table writes of the lanes up to it are committed, later lanes
+//    are discarded -- exactly the state the serial loop would leave.
+//  * match extension (snappy.c:163-164): 64 byte-compares per step, the
+//    first mismatch found by ballot.
+//  * post-copy re-probe, including lcdb's 64-bit compare (snappy.c:172-186):
+//    scalar.
+//  * emission (snappy.c:53-102): header bytes and literal bytes written by
+//    lanes straight to the output.
+#include "lgs_device.h"
+#include "lgs_launch.h"
+
+namespace lgs {
+
+__constant__ ProbeTable kProbe = ProbeTable();
+
+// snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o.
+// Returns bytes written.
+__device__ __forceinline__ uint32_t emit_literal(uint8_t* o, const uint8_t* in,
+                                                 uint32_t from, uint32_t len) {
+  const uint32_t lane = lane_id();
+  const uint32_t m = len - 1;
+  const uint32_t hl = m < 60 ? 1u : (m < 256 ? 2u : 3u);
+  if (lane < hl) {
+    uint8_t b;
+    if (lane == 0) b = m < 60 ? (uint8_t)(m << 2) : (m < 256 ? (uint8_t)0xf0 : (uint8_t)0xf4);
+    else if (lane == 1) b = (uint8_t)(m & 0xffu);
+    else b = (uint8_t)(m >> 8);
+    o[lane] = b;
+  }
+  for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
+    const uint32_t j = j0 + lane;
+    if (j < len) o[hl + j] = in[from + j];
+  }
+  return hl + len;
+}
+
+// snappy.c:75-102: 64-byte COPY2 pieces while len >= 68, a 60-byte COPY2 if
+// then len > 64, then COPY2 (len >= 12 or dist >= 2048) or COPY1.
+__device__ __forceinline__ uint32_t emit_copy(uint8_t* o, uint32_t dist, uint32_t len) {
+  const uint32_t lane = lane_id();
+  const uint32_t n64 = len >= 68 ? (len - 68) / 64 + 1 : 0;
+  uint32_t rest = len - 64 * n64;
+  const uint32_t has60 = rest > 64 ? 1u : 0u;
+  rest -= 60 * has60;
+  const bool c1 = rest < 12 && dist < 2048;
+  const uint32_t head = 3 * (n64 + has60);
+  const uint32_t total = head + (c1 ? 2u : 3u);
+  const uint8_t lo = (uint8_t)(dist & 0xffu), hi = (uint8_t)((dist >> 8) & 0xffu);
+  for (uint32_t b = lane; b < total; b += kWave) {
+    uint8_t v;
+    if (b < head) {
+      const uint32_t r = b % 3;
+      const bool is60 = has60 && b >= 3 * n64;
+      v = r == 0 ? (is60 ? (uint8_t)0xee : (uint8_t)0xfe) : (r == 1 ? lo : hi);
+    } else {
+      const uint32_t r = b - head;
+      if (c1) v = r == 0 ? (uint8_t)(((dist >> 8) << 5) | ((rest - 4) << 2) | 1u) : lo;
+      else v = r == 0 ? (uint8_t)(((rest - 1) << 2) | 2u) : (r == 1 ? lo : hi);
+    }
+    o[b] = v;
+  }
+  return total;
+}
+
+// Encode one chunk x[0..n), 17 <= n <= 65536, held in LDS.  `tab` is the
+// u16 hash table, `lid` a u8 scratch of 2048 entries.  Writes to o, returns
+// bytes written.  Mirrors snappy.c:104-195 step for step.
+__device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, uint8_t* lid,
+                                 uint8_t* o) {
+  const uint32_t lane = lane_id();
+  const uint32_t last = n - kMargin;                  // snappy.c:106
+
+  uint32_t tsize = 256, shift = 24;                   // snappy.c:108-125
+  while (tsize < kTableCap && tsize < n) {
+    tsize <<= 1;
+    --shift;
+  }
+  for (uint32_t e = lane; e < tsize; e += kWave) tab[e] = 0;   // snappy.c:129
+  order();
+
+  uint32_t op = 0;       // output cursor
+  uint32_t lit = 0;      // first byte not yet emitted (snappy.c:111 "emit")
+  uint32_t at = 1;       // snappy.c:112
+  uint32_t ref = 0;
+
+  for (;;) {
+    // ---- literal search from `at` (snappy.c:133-154), 64 probes a step.
+    const uint32_t start = at;
+    uint32_t k = 0;
+    bool found = false;
+    for (;;) {
+      const uint32_t kk = k + lane;
+      const uint32_t kc = kk < kProbeTab ? kk : kProbeTab - 1;
+      const uint32_t p = start + kProbe.off[kc];
+      const uint32_t pn = start + kProbe.off[kc + 1];
+      const bool valid = kk < kProbeTab && pn <= last;            // snappy.c:143
+      const uint64_t vm = __ballot(valid);
+      const uint32_t nvalid = vm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~vm);
+
+      uint32_t h = 0, xv = 0;
+      if (valid) {
+        xv = lds_ld32(x, p);
+        h = hash32(xv, shift);
+        lid[h] = (uint8_t)lane;
+      }
+      order();
+      const bool loser = valid && lid[h] != lane;
+      const uint64_t lm = __ballot(loser);
+      const uint32_t first_loser = lm ? (uint32_t)__builtin_ctzll(lm) : 64u;
+      const uint32_t nsafe = first_loser > 1 ? first_loser : 1u;
+      const uint32_t nproc = nsafe < nvalid ? nsafe : nvalid;
+      if (nproc == 0) goto tail;                                  // first probe past limit
+
+      const bool act = lane < nproc;
+      uint32_t cand = 0;
+      bool match = false;
+      if (act) {
+        cand = tab[h];                                            // snappy.c:146
+        match = xv == lds_ld32(x, cand);                          // snappy.c:152
+      }
+      const uint64_t mm = __ballot(act && match);
+      const uint32_t ncommit = mm ? (uint32_t)__builtin_ctzll(mm) + 1 : nproc;
+      if (lane < ncommit) tab[h] = (uint16_t)p;                   // snappy.c:148
+      order();
+      if (mm) {
+        const uint32_t m = ncommit - 1;
+        at = uni(__shfl(p, m));
+        ref = uni(__shfl(cand, m));
+        found = true;
+        break;
+      }
+      if (nproc < nsafe) goto tail;                               // next probe past limit
+      k += nproc;
+    }
+    (void)found;
+
+    op += emit_literal(o + op, x, lit, at - lit);                 // snappy.c:156
+
+    // ---- copies, with lcdb's immediate re-match (snappy.c:158-187).
+    for (;;) {
+      const uint32_t base = at;
+      uint32_t r = ref + 4;
+      at += 4;
+      for (;;) {                                                  // snappy.c:163-164
+        const uint32_t q = at + lane;
+        const bool same = q < n && x[r + lane] == x[q];
+        const uint64_t diff = __ballot(!same);
+        if (diff) {
+          at += (uint32_t)__builtin_ctzll(diff);
+          break;
+        }
+        at += kWave;
+        r += kWave;
+      }
+      at = uni(at);
+
+      op += emit_copy(o + op, base - ref, at - base);             // snappy.c:166
+      lit = at;
+      if (at >= last) goto tail;                                  // snappy.c:169
+
+      const uint64_t w = uni64(lds_ld64(x, at - 1));              // snappy.c:172
+      if (lane == 0) tab[hash32((uint32_t)w, shift)] = (uint16_t)(at - 1);
+      order();
+      const uint32_t cur = hash32((uint32_t)(w >> 8), shift);     // snappy.c:177
+      ref = uni(tab[cur]);
+      order();
+      if (lane == 0) tab[cur] = (uint16_t)at;
+      order();
+      // lcdb's 64-bit compare (snappy.c:182): bytes at..at+6 against a
+      // zero-extended 4-byte load.
+      if ((w >> 8) != (uint64_t)uni(lds_ld32(x, ref))) {
+        ++at;
+        break;
+      }
+    }
+  }
+
+tail:
+  if (lit < n) op += emit_literal(o + op, x, lit, n - lit);        // snappy.c:190-192
+  return op;
+}
+
+// Work item i: input in[in_off[i] .. + in_len[i]) (<= 64 KiB), output at
+// out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
+// its varint32 length (snappy.c:368).  Otherwise hdr[i] is the varint value
+// to prefix, or 0xffffffff for none (a later chunk of a > 64 KiB block).
+template <uint32_t IN_CAP, uint32_t WAVES>
+__global__ __launch_bounds__(64 * WAVES) void encode_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
+  __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lid[WAVES][kTableCap];
+
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t slot = blockIdx.x * WAVES + wv;
+  if (slot >= n) return;
+  const uint32_t i = index ? index[slot] : slot;
+  const uint32_t lane = lane_id();
+
+  const uint32_t len = in_len[i];
+  uint8_t* o = out + out_off[i];
+  const uint32_t sh = stage_in(&s_in[wv][0], in + in_off[i], len);
+  const uint8_t* x = &s_in[wv][sh];
+  order();
+
+  // varint32 header, coding.h:140-167.
+  const uint32_t hv = hdr ? hdr[i] : len;
+  uint32_t op = 0;
+  if (hv != 0xffffffffu) {
+    const uint32_t hl = hv < (1u << 7) ? 1 : hv < (1u << 14) ? 2 : hv < (1u << 21) ? 3
+                      : hv < (1u << 28) ? 4 : 5;
+    if (lane < hl) {
+      uint32_t b = (hv >> (7 * lane)) & 0x7fu;
+      if (lane + 1 < hl) b |= 0x80u;
+      o[lane] = (uint8_t)b;
+    }
+    op = hl;
+  }
+
+  if (len >= kMinBlock) {
+    op += encode_chunk(x, len, &s_tab[wv][0], &s_lid[wv][0], o + op);
+  } else if (len > 0) {
+    op += emit_literal(o + op, x, 0, len);                       // snappy.c:379-380
+  }
+  if (lane == 0) out_len[i] = op;
+}
+
+// Gather kernel for > 64 KiB blocks: piece p (one chunk's encoded bytes,
+// src + src_off[p], src_len[p]) is appended at dst + dst_off[p].
+__global__ __launch_bounds__(256) void concat_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, uint32_t n) {
+  const uint32_t p = blockIdx.x;
+  if (p >= n) return;
+  const uint8_t* s = src + src_off[p];
+  uint8_t* d = dst + dst_off[p];
+  const uint32_t len = src_len[p];
+  for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) d[j] = s[j];
+}
+
+template <uint32_t IN_CAP, uint32_t WAVES>
+static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
+  const uint32_t grid = (a.n + WAVES - 1) / WAVES;
+  hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
+                     a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n);
+  return hipGetLastError();
+}
+
+constexpr uint32_t kEncCap0 = 4608;
+constexpr uint32_t kEncCap1 = 16896;
+constexpr uint32_t kEncCap2 = 65536;
+
+// max_in: largest item length in the launch (<= 65536).
+hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
+  if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
+  if (max_in <= kEncCap2) return launch_encode_cls<kEncCap2, 1>(a, s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                         uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(concat_kernel, dim3(n), dim3(256), 0, s, src, src_off, src_len, dst,
+                     dst_off, n);
+  return hipGetLastError();
+}
+
+}  // namespace lgs

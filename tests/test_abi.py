@@ -1,0 +1,69 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares;
+host-only entry points (size bound, size header) match the oracle.  No GPU
+compute happens here."""
+from __future__ import annotations
+
+import glob
+import os
+import re
+import subprocess
+
+import oracle
+from lcdb_amd import _native, build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared() -> set[str]:
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\([^;{]*\)\s*;", text, re.M):
+            names.add(m.group(1))
+    return names
+
+
+def _dynsyms(path: str) -> set[str]:
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def test_header_declares_dropin_and_batch():
+    d = _declared()
+    for name in ("ldb_snappy_encode_size", "ldb_snappy_encode", "ldb_snappy_decode_size",
+                 "ldb_snappy_decode", "lgs_encode_batch_dev", "lgs_decode_batch_dev"):
+        assert name in d
+    assert d == set(_native.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    syms = _dynsyms(build.LIB)
+    missing = _declared() - syms
+    assert not missing, missing
+    lib = _native.lib()
+    for name in _declared():
+        assert getattr(lib, name) is not None
+
+
+def test_product_does_not_link_the_oracle():
+    syms = _dynsyms(build.LIB)
+    assert not any(s.startswith(("oracle_", "cpu_batch")) for s in syms)
+    ldd = subprocess.run(["ldd", build.LIB], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd and "libref_snappy" not in ldd
+
+
+def test_gfx950_code_object():
+    blob = open(build.LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"--gfx9" not in blob.replace(b"--gfx950", b"")   # gfx950 only
+
+
+def test_host_side_size_functions_match_oracle(vectors):
+    from lcdb_amd import snappy  # loads the library; size calls need no GPU
+    orc = oracle.restatement()
+    for n in (0, 1, 16, 17, 4096, 65536, 1 << 20, 0x7FFFFFFF, 0x80000000, 1 << 40):
+        assert snappy.encode_size(n) == orc.encode_size(n)
+    for v in vectors:
+        s = v.a if v.kind == 1 else v.b
+        assert snappy.decode_size(s) == orc.decode_size(s), v.name

@@ -1,0 +1,197 @@
+"""GPU parity: the HIP codec (through the C ABI) against the reference's
+golden vectors and the oracle.  Bit-exact: compressed bytes identical to the
+reference encoder, decoded bytes identical, accept/reject identical."""
+from __future__ import annotations
+
+import hashlib
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from lcdb_amd import corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dropin_encode_golden(gpu, vectors):
+    for v in vectors:
+        if v.kind == 0:
+            assert gpu.encode(v.a) == v.b, v.name
+
+
+def test_dropin_decode_golden(gpu, vectors):
+    for v in vectors:
+        if v.kind == 0:
+            assert gpu.decode(v.b) == v.a, v.name
+        else:
+            out = gpu.decode(v.a)
+            assert (out is not None) == bool(v.ok), v.name
+            if v.ok:
+                assert out == v.b, v.name
+
+
+def test_dropin_ramp_known_answer(gpu, digests):
+    # t-snappy.c:24-53 (1 MiB input: 16 chunks of 64 KiB, concatenated on device)
+    data = bytes(i & 0xFF for i in range(1 << 20))
+    enc = gpu.encode(data)
+    assert len(enc) == 53203
+    assert hashlib.sha256(enc).hexdigest() == digests["ramp_1MiB"]["comp_sha256"]
+    assert gpu.decode_size(enc) == 1 << 20
+    assert gpu.decode(enc) == data
+
+
+def test_batch_host_golden(gpu, vectors):
+    enc = [v for v in vectors if v.kind == 0 and len(v.a) <= 65536]
+    outs = gpu.encode_batch_host([v.a for v in enc])
+    for v, o in zip(enc, outs):
+        assert o == v.b, v.name
+    res, st = gpu.decode_batch_host([v.b for v in enc], [len(v.a) for v in enc])
+    for v, o, s in zip(enc, res, st):
+        assert s == gpu.LGS_ST_OK and o == v.a, v.name
+    dec = [v for v in vectors if v.kind == 1]
+    caps = [len(v.b) if v.ok else 4096 for v in dec]
+    res, st = gpu.decode_batch_host([v.a for v in dec], caps)
+    for v, o, s in zip(dec, res, st):
+        if v.ok:
+            assert s == gpu.LGS_ST_OK and o == v.b, v.name
+        else:
+            # a reject may also be reported as "no space" when the bogus
+            # header exceeds the slot; never as ok
+            assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), v.name
+
+
+def test_decode_nospace(gpu):
+    raw = corpus.fillseq(1).block(0)
+    comp = gpu.encode(raw)
+    res, st = gpu.decode_batch_host([comp, comp], [len(raw) - 1, len(raw)])
+    assert list(st) == [gpu.LGS_ST_NOSPACE, gpu.LGS_ST_OK]
+    assert res[1] == raw
+
+
+def _device_roundtrip(c: corpus.Corpus):
+    import torch
+    from lcdb_amd import batch
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    out = batch.decode_slots(c.len)
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    batch.decode(comp, out, st)
+    torch.cuda.synchronize()
+    return raw, comp, out, st
+
+
+def test_device_batch_c1_fillseq(gpu, digests):
+    d = digests["C1_fillseq_1024x4KiB"]
+    c = corpus.fillseq(1024)
+    from lcdb_amd import batch
+    raw, comp, out, st = _device_roundtrip(c)
+    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"])
+    assert bool((st == 1).all())
+    assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"])
+
+
+def test_device_batch_c3_mixed(gpu, digests):
+    d = digests["C3_mixed"]
+    c = corpus.mixed()
+    from lcdb_amd import batch
+    raw, comp, out, st = _device_roundtrip(c)
+    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"])
+    assert bool((st == 1).all())
+    assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"])
+
+
+def test_device_batch_c2_full_size(gpu, digests):
+    # BASELINE config 2 at full size: 65 536 fillseq blocks; checksum of the
+    # whole compressed corpus equals the reference's, round trip is exact.
+    d = digests["C2_fillseq_65536x4KiB"]
+    c = corpus.fillseq(65536)
+    from lcdb_amd import batch
+    raw, comp, out, st = _device_roundtrip(c)
+    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"])
+    assert int(st.sum().item()) == c.n
+    assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"])
+
+
+def test_device_batch_unaligned_offsets(gpu):
+    import torch
+    from lcdb_amd import batch
+    c0 = corpus.concat(corpus.fillseq(37), corpus.random_blocks(11, 4096), corpus.fillseq(5, 16384))
+    # re-pack with odd offsets: block i at 7*i + running total
+    blocks = c0.blocks()
+    off = np.zeros(len(blocks), dtype=np.uint64)
+    at = 3
+    for i, b in enumerate(blocks):
+        off[i] = at
+        at += len(b) + (i % 13)
+    buf = np.zeros(at + 32, dtype=np.uint8)
+    for i, b in enumerate(blocks):
+        buf[int(off[i]):int(off[i]) + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    c = corpus.Corpus(buf, off, c0.len.copy())
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    comp.off += torch.arange(c.n, device="cuda", dtype=torch.int64) % 7   # odd out slots
+    comp.buf = torch.empty(comp.buf.numel() + 16, dtype=torch.uint8, device="cuda")
+    batch.encode(raw, comp)
+    torch.cuda.synchronize()
+    ref = oracle.best()
+    hc = batch.to_host(comp)
+    for i in range(c.n):
+        assert hc.block(i) == ref.encode(blocks[i]), i
+    out = batch.decode_slots(c.len + 16)   # room for the odd shifts below
+    out.off += (torch.arange(c.n, device="cuda", dtype=torch.int64) * 5) % 16
+    out.buf = torch.empty(out.buf.numel() + 16, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    batch.decode(comp, out, st)
+    torch.cuda.synchronize()
+    ho = batch.to_host(out)
+    assert bool((st == 1).all())
+    for i in range(c.n):
+        assert ho.block(i) == blocks[i], i
+
+
+def test_dropin_concurrent_threads(gpu):
+    c = corpus.fillseq(64)
+    ref = oracle.best()
+    want = [ref.encode(b) for b in c.blocks()]
+    errors = []
+
+    def work(k):
+        try:
+            for i in range(k, c.n, 4):
+                e = gpu.encode(c.block(i))
+                if e != want[i] or gpu.decode(e) != c.block(i):
+                    errors.append(i)
+        except Exception as exc:   # pragma: no cover - reported below
+            errors.append(repr(exc))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:5]
+
+
+def test_random_inputs_vs_oracle(gpu):
+    import random
+    rng = random.Random(7)
+    ref = oracle.best()
+    blocks = []
+    for _ in range(300):
+        n = rng.choice([rng.randrange(0, 40), rng.randrange(40, 4096), rng.randrange(4096, 65537)])
+        kind = rng.randrange(3)
+        if kind == 0:
+            b = bytes(rng.randrange(256) for _ in range(n))
+        elif kind == 1:
+            alpha = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 5)))
+            b = bytes(rng.choice(alpha) for _ in range(n))
+        else:
+            unit = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 30)))
+            b = (unit * (n // max(1, len(unit)) + 1))[:n]
+        blocks.append(b)
+    outs = gpu.encode_batch_host(blocks)
+    for b, o in zip(blocks, outs):
+        assert o == ref.encode(b)
