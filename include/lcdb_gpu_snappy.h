@@ -65,18 +65,15 @@ int ldb_snappy_decode(uint8_t *zp, const uint8_t *xp, size_t xn);
 #define LGS_ST_OK       1
 #define LGS_ST_NOSPACE  2   /* decoded length > out_cap[i]              */
 
-/* Largest block length the batch encoder accepts per block.  Larger inputs
-   go through ldb_snappy_encode (chunked). */
-#define LGS_MAX_BATCH_BLOCK 65536u
-
 /* Worst-case encoded size (same formula as ldb_snappy_encode_size). */
 size_t lgs_encode_bound(size_t n);
 
 /* Device-resident encode.  All pointers are device pointers.  Block i is
-   d_in[d_in_off[i] .. + d_in_len[i]) (each <= LGS_MAX_BATCH_BLOCK); its
-   encoding is written at d_out + d_out_off[i] (room for
-   lgs_encode_bound(d_in_len[i]) bytes) and its length to d_out_len[i].
-   max_in_len >= every d_in_len[i] (selects the LDS class).  Asynchronous on
+   d_in[d_in_off[i] .. + d_in_len[i]) (any length < 2^31; blocks over
+   64 KiB are encoded as consecutive 64 KiB chunks by one wave, exactly as
+   snappy.c:370-381 does); its encoding is written at d_out + d_out_off[i]
+   (room for lgs_encode_bound(d_in_len[i]) bytes) and its length to
+   d_out_len[i].  max_in_len >= every d_in_len[i] (selects the LDS class).  Asynchronous on
    `stream` (a hipStream_t, NULL = default stream). */
 int lgs_encode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
                          const uint32_t *d_in_len, uint8_t *d_out,

@@ -12,7 +12,6 @@ from .build import LIB
 
 LGS_OK = 0
 LGS_ST_CORRUPT, LGS_ST_OK, LGS_ST_NOSPACE = 0, 1, 2
-LGS_MAX_BATCH_BLOCK = 65536
 
 _u8p = C.POINTER(C.c_uint8)
 _vp = C.c_void_p
@@ -44,6 +43,13 @@ def lib() -> C.CDLL:
     """Load (once) and return the native library; raises if it is absent."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: torch's wheel bundles its own
+        # libamdhip64/libhsa-runtime64 and its libraries NEED the unversioned
+        # "libamdhip64.so", while ours NEEDs the soname "libamdhip64.so.7".
+        # Loading torch first makes our NEEDED entries resolve (by soname) to
+        # the runtime torch already loaded; loading ours first would make
+        # torch bring up a second HSA runtime that then finds no GPU.
+        import torch  # noqa: F401
         if not os.path.exists(LIB):
             raise ImportError(
                 f"lcdb_amd native library not built: {LIB} is missing "

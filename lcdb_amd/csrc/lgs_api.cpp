@@ -321,8 +321,7 @@ int lgs_encode_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const ui
   if (n == 0) return LGS_OK;
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len)
     return fail(LGS_EINVAL, "NULL argument");
-  if (max_in_len > LGS_MAX_BATCH_BLOCK)
-    return fail(LGS_EINVAL, "max_in_len %u > %u", max_in_len, LGS_MAX_BATCH_BLOCK);
+  if (max_in_len > 0x7fffffffu) return fail(LGS_EINVAL, "max_in_len %u too large", max_in_len);
   EncodeArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nullptr, nullptr, n};
   LGS_HIP(launch_encode(a, max_in_len, (hipStream_t)stream));
   return LGS_OK;
@@ -352,8 +351,7 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   size_t in_total = 0, out_total = 0;
   uint32_t max_in = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    if (in_len[i] > LGS_MAX_BATCH_BLOCK)
-      return fail(LGS_EINVAL, "block %u: %u bytes > %u", i, in_len[i], LGS_MAX_BATCH_BLOCK);
+    if (in_len[i] > 0x7fffffffu) return fail(LGS_EINVAL, "block %u too large", i);
     in_total += align_up(in_len[i], 16);
     out_total += align_up(bound_of(in_len[i]), 16);
     if (in_len[i] > max_in) max_in = in_len[i];

@@ -20,17 +20,10 @@
 
 namespace lgs {
 
-// Byte source over an LDS-staged stream (byte k at base[k]).
-struct LdsStream {
-  const uint8_t* base;
-  __device__ uint64_t win(uint32_t pos) const { return uni64(lds_ld64(base, pos)); }
-  __device__ uint8_t byte(uint32_t pos) const { return base[pos]; }
-};
-
 // Byte source over the stream in global memory (oversized blocks only).
 // Window bytes at or past `len` read as zero and are never consumed.
 struct GlobalStream {
-  const uint8_t* base;
+  gptr<const uint8_t> base;
   uint32_t len;
   __device__ uint64_t win(uint32_t pos) const {
     uint64_t v = 0;
@@ -41,7 +34,9 @@ struct GlobalStream {
   __device__ uint8_t byte(uint32_t pos) const { return base[pos]; }
 };
 
-// Decode one stream into `o` (LDS).  Returns 1 ok / 0 corrupt / 2 too big.
+// Decode one stream held in global memory (blocks whose compressed length
+// exceeds the LDS staging area) into `o` (LDS).  Returns 1 ok / 0 corrupt /
+// 2 too big.
 template <class Src>
 __device__ uint32_t decode_stream(const Src& src, uint32_t slen, uint8_t* o,
                                   uint32_t cap, uint32_t* want_out) {
@@ -137,18 +132,130 @@ __device__ uint32_t decode_stream(const Src& src, uint32_t slen, uint8_t* o,
   return made == want ? 1u : 0u;                    // snappy.c:337
 }
 
-// Stream the decoded bytes o[shift .. shift+len) (LDS) to dst, where
-// shift == dst & 15: every full granule is one 16-byte store.
-__device__ __forceinline__ void flush_out(uint8_t* dst, const uint8_t* o, uint32_t len) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
-  const uint32_t shift = (uint32_t)(a & 15u);
-  uint8_t* g = reinterpret_cast<uint8_t*>(a - shift);
+// Fast path for an LDS-staged stream: stream byte k sits at base[sh + k]
+// (base 16-byte aligned).  The tag walk never waits on LDS: a 256-byte
+// window of the stream lives in one VGPR (lane l holds dword wbase + l) and
+// each tag's 8-byte view is two v_readlane + a 64-bit shift into SGPRs.  The
+// window is refilled (one ds_read_b32 per lane) every ~250 stream bytes.
+// Only the byte moves touch LDS, one read + one write per tag.
+__device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, uint8_t* o,
+                               uint32_t cap, uint32_t* want_out) {
+  const uint32_t lane = lane_id();
+  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);
+  uint32_t wbase = sh >> 2;
+  uint32_t win = b32[wbase + lane];
+
+  auto view = [&](uint32_t apos) -> uint64_t {     // bytes apos..apos+4 (>= 5 valid)
+    uint32_t d = (apos >> 2) - wbase;
+    if (d >= 63) {
+      wbase = apos >> 2;
+      win = b32[wbase + lane];
+      d = 0;
+    }
+    const uint32_t lo = __builtin_amdgcn_readlane(win, d);
+    const uint32_t hi = __builtin_amdgcn_readlane(win, d + 1);
+    return ((((uint64_t)hi) << 32) | lo) >> ((apos & 3u) * 8);
+  };
+
+  // varint32 header, coding.h:169-204.
+  const uint64_t w = view(sh);
+  uint32_t want = 0, hlen = 0;
+  for (uint32_t i = 0; i < 5 && i < slen; ++i) {
+    const uint32_t b = (uint32_t)(w >> (8 * i)) & 0xffu;
+    if ((b & 0x80u) == 0) {
+      want |= b << (7 * i);
+      hlen = i + 1;
+      break;
+    }
+    want |= (b & 0x7fu) << (7 * i);
+  }
+  if (hlen == 0 || want > 0x7fffffffu) return 0;    // snappy.c:405-409
+  if (want > cap) return 2;
+  *want_out = want;
+
+  uint32_t apos = sh + hlen;                        // absolute LDS offset of the next tag
+  const uint32_t aend = sh + slen;
+  uint32_t made = 0;
+
+  while (apos < aend) {                             // snappy.c:208
+    const uint64_t t = view(apos);
+    const uint32_t tag = (uint32_t)t & 0xffu;
+    const uint32_t left = aend - apos;
+
+    if ((tag & 3u) == 0) {                          // literal, snappy.c:210-273
+      uint32_t m = tag >> 2, hl = 1;
+      if (m >= 60) {
+        const uint32_t extra = m - 59;
+        if (left - 1 < extra) return 0;
+        const uint32_t hi = (uint32_t)(t >> 8);
+        m = extra == 4 ? hi : (hi & ((1u << (8 * extra)) - 1u));
+        hl += extra;
+      }
+      if (m >= 0x7fffffffu) return 0;               // snappy.c:258
+      const uint32_t len = m + 1;
+      if (len > want - made || len > left - hl) return 0;   // snappy.c:263
+      const uint32_t from = apos + hl;
+      if (len <= kWave) {
+        if (lane < len) o[made + lane] = base[from + lane];
+      } else {
+        for (uint32_t j = lane; j < len; j += kWave) o[made + j] = base[from + j];
+      }
+      order();
+      made += len;
+      apos = from + len;
+      continue;
+    }
+
+    uint32_t len, dist, hl;
+    if ((tag & 3u) == 1) {                          // COPY1, snappy.c:276-287
+      if (left < 2) return 0;
+      len = 4 + ((tag >> 2) & 7u);
+      dist = ((tag & 0xe0u) << 3) | ((uint32_t)(t >> 8) & 0xffu);
+      hl = 2;
+    } else if ((tag & 3u) == 2) {                   // COPY2, snappy.c:289-301
+      if (left < 3) return 0;
+      len = 1 + (tag >> 2);
+      dist = (uint32_t)(t >> 8) & 0xffffu;
+      hl = 3;
+    } else {                                        // COPY4, snappy.c:303-317
+      if (left < 5) return 0;
+      len = 1 + (tag >> 2);
+      dist = (uint32_t)(t >> 8);
+      hl = 5;
+    }
+    apos += hl;
+    if (dist == 0 || dist >= 0x80000000u) return 0;   // snappy.c:320
+    if (made < dist || len > want - made) return 0;   // snappy.c:323
+    // len <= 64.  dist >= len: a plain move.  dist < len (rare): the
+    // reference's forward byte loop repeats the dist-byte pattern.
+    if (dist >= len) {
+      if (lane < len) {
+        const uint8_t v = o[made - dist + lane];
+        o[made + lane] = v;
+      }
+    } else if (lane < len) {
+      const uint8_t v = o[made - dist + lane % dist];
+      o[made + lane] = v;
+    }
+    order();
+    made += len;
+  }
+
+  return made == want ? 1u : 0u;                    // snappy.c:337
+}
+
+// Stream the decoded bytes lds[shift .. shift+len) to dst, where
+// shift == dst & 15 (lds is the 16-byte aligned base of the output image):
+// every full granule is one 16-byte store.
+__device__ __forceinline__ void flush_out(gptr<uint8_t> dst, const uint8_t* o, uint32_t len) {  // o: LDS base
+  const uint32_t shift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+  const gptr<uint8_t> g = dst - shift;
   const uint32_t end = shift + len;
   const uint32_t n16 = (end + 15u) >> 4;
   for (uint32_t c = lane_id(); c < n16; c += kWave) {
     const uint32_t lo = c << 4, hi = lo + 16;
     if (lo >= shift && hi <= end) {
-      *reinterpret_cast<uint4*>(g + lo) = *reinterpret_cast<const uint4*>(o + lo);
+      *(gptr<u32x4>)(g + lo) = *reinterpret_cast<const u32x4*>(o + lo);
     } else {
       for (uint32_t b = lo; b < hi; ++b)
         if (b >= shift && b < end) g[b] = o[b];
@@ -163,18 +270,22 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
     const uint32_t* __restrict__ index, uint32_t n) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
+  // s_in: + 48 for the alignment shift and zero pad, + 256 so the VGPR
+  // window of decode_lds never reads past this array.
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48 + 256];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][OUT_CAP + 32];
 
-  const uint32_t wv = threadIdx.x >> 6;
+  // Per-wave scalars go through v_readfirstlane so hipcc keeps the whole
+  // tag walk on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
+  const uint32_t wv = uni(threadIdx.x >> 6);
   const uint32_t slot = blockIdx.x * WAVES + wv;
   if (slot >= n) return;
-  const uint32_t i = index ? index[slot] : slot;
+  const uint32_t i = uni(index ? index[slot] : slot);
 
-  const uint8_t* src = in + in_off[i];
-  const uint32_t slen = in_len[i];
-  uint8_t* dst = out + out_off[i];
-  const uint32_t cap = out_cap[i] < OUT_CAP ? out_cap[i] : OUT_CAP;
+  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
+  const uint32_t slen = uni(in_len[i]);
+  const gptr<uint8_t> dst = to_global(out) + uni64(out_off[i]);
+  const uint32_t cap = uni(out_cap[i] < OUT_CAP ? out_cap[i] : OUT_CAP);
   const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
   uint8_t* o = &s_out[wv][oshift];
 
@@ -182,11 +293,11 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   if (slen <= IN_CAP) {
     const uint32_t sh = stage_in(&s_in[wv][0], src, slen);
     order();
-    st = decode_stream(LdsStream{&s_in[wv][sh]}, slen, o, cap, &want);
+    st = decode_lds(&s_in[wv][0], sh, slen, o, cap, &want);
   } else {
     st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
   }
-  if (st == 1) flush_out(dst, o, want);
+  if (st == 1) flush_out(dst, &s_out[wv][0], want);
   if (lane_id() == 0) {
     status[i] = (uint8_t)st;
     out_len[i] = st == 1 ? want : 0;
@@ -213,7 +324,7 @@ __global__ __launch_bounds__(64) void decode_big_kernel(
   if (slot >= n) return;
   const uint32_t i = index ? index[slot] : slot;
   const uint32_t lane = lane_id();
-  const GlobalStream src{in + in_off[i], in_len[i]};
+  const GlobalStream src{to_global(in) + in_off[i], in_len[i]};
   const uint32_t slen = in_len[i];
   uint8_t* o = out + out_off[i];
   const uint32_t cap = out_cap[i];

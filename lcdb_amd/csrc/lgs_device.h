@@ -35,6 +35,23 @@ struct ProbeTable {
   }
 };
 
+// Global-memory pointers.  Offsets added to a kernel-argument pointer after a
+// v_readfirstlane keep hipcc's address-space inference; casting through an
+// integer does not, and flat_* accesses also count on lgkmcnt (so every LDS
+// wait would wait for them too).  Everything that touches HBM goes through
+// these types.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+
+// 16-byte vector (a plain clang vector: HIP's uint4 struct has no
+// address-space-qualified assignment).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <class T>
+__device__ __forceinline__ gptr<T> to_global(T* p) {
+  return (gptr<T>)p;
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kWave - 1); }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) {
@@ -79,15 +96,14 @@ __device__ __forceinline__ uint64_t lds_ld64(const uint8_t* base, uint32_t at) {
 // lane moves one aligned 16-byte granule.  Returns the LDS shift (src & 15).
 // Reads may touch the aligned 16-byte granules that contain the first and
 // last byte, never a different page.
-__device__ __forceinline__ uint32_t stage_in(uint8_t* lds, const uint8_t* src, uint32_t len) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
-  const uint32_t shift = (uint32_t)(a & 15u);
-  const uint4* g = reinterpret_cast<const uint4*>(a - shift);
-  uint4* l = reinterpret_cast<uint4*>(lds);
+__device__ __forceinline__ uint32_t stage_in(uint8_t* lds, gptr<const uint8_t> src, uint32_t len) {
+  const uint32_t shift = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15u);
+  gptr<const u32x4> g = (gptr<const u32x4>)(src - shift);
+  u32x4* l = reinterpret_cast<u32x4*>(lds);
   const uint32_t n16 = (shift + len + 15u) >> 4;
   for (uint32_t c = lane_id(); c < n16; c += kWave) l[c] = g[c];
   // Zero pad one granule past the end so fixed-width window reads are defined.
-  if (lane_id() == 0) l[n16] = make_uint4(0, 0, 0, 0);
+  if (lane_id() == 0) l[n16] = u32x4{0, 0, 0, 0};
   return shift;
 }
 

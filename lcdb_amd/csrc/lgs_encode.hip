@@ -32,7 +32,7 @@ __constant__ ProbeTable kProbe = ProbeTable();
 
 // snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o.
 // Returns bytes written.
-__device__ __forceinline__ uint32_t emit_literal(uint8_t* o, const uint8_t* in,
+__device__ __forceinline__ uint32_t emit_literal(gptr<uint8_t> o, const uint8_t* in,
                                                  uint32_t from, uint32_t len) {
   const uint32_t lane = lane_id();
   const uint32_t m = len - 1;
@@ -44,6 +44,7 @@ __device__ __forceinline__ uint32_t emit_literal(uint8_t* o, const uint8_t* in,
     else b = (uint8_t)(m >> 8);
     o[lane] = b;
   }
+#pragma clang loop unroll(disable) vectorize(disable)
   for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
     const uint32_t j = j0 + lane;
     if (j < len) o[hl + j] = in[from + j];
@@ -52,8 +53,9 @@ __device__ __forceinline__ uint32_t emit_literal(uint8_t* o, const uint8_t* in,
 }
 
 // snappy.c:75-102: 64-byte COPY2 pieces while len >= 68, a 60-byte COPY2 if
-// then len > 64, then COPY2 (len >= 12 or dist >= 2048) or COPY1.
-__device__ __forceinline__ uint32_t emit_copy(uint8_t* o, uint32_t dist, uint32_t len) {
+// then len > 64, then COPY2 (len >= 12 or dist >= 2048) or COPY1.  Lane b
+// writes byte b of the emitted sequence.
+__device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, uint32_t len) {
   const uint32_t lane = lane_id();
   const uint32_t n64 = len >= 68 ? (len - 68) / 64 + 1 : 0;
   uint32_t rest = len - 64 * n64;
@@ -63,28 +65,51 @@ __device__ __forceinline__ uint32_t emit_copy(uint8_t* o, uint32_t dist, uint32_
   const uint32_t head = 3 * (n64 + has60);
   const uint32_t total = head + (c1 ? 2u : 3u);
   const uint8_t lo = (uint8_t)(dist & 0xffu), hi = (uint8_t)((dist >> 8) & 0xffu);
-  for (uint32_t b = lane; b < total; b += kWave) {
-    uint8_t v;
-    if (b < head) {
-      const uint32_t r = b % 3;
-      const bool is60 = has60 && b >= 3 * n64;
-      v = r == 0 ? (is60 ? (uint8_t)0xee : (uint8_t)0xfe) : (r == 1 ? lo : hi);
-    } else {
-      const uint32_t r = b - head;
-      if (c1) v = r == 0 ? (uint8_t)(((dist >> 8) << 5) | ((rest - 4) << 2) | 1u) : lo;
-      else v = r == 0 ? (uint8_t)(((rest - 1) << 2) | 2u) : (r == 1 ? lo : hi);
+  const uint8_t last0 = c1 ? (uint8_t)(((dist >> 8) << 5) | ((rest - 4) << 2) | 1u)
+                           : (uint8_t)(((rest - 1) << 2) | 2u);
+#pragma clang loop unroll(disable) vectorize(disable)
+  for (uint32_t b0 = 0; b0 < total; b0 += kWave) {
+    const uint32_t b = b0 + lane;
+    if (b < total) {
+      uint8_t v;
+      if (b < head) {
+        const uint32_t r = b % 3;
+        const bool is60 = has60 && b >= 3 * n64;
+        v = r == 0 ? (is60 ? (uint8_t)0xee : (uint8_t)0xfe) : (r == 1 ? lo : hi);
+      } else {
+        const uint32_t r = b - head;
+        v = r == 0 ? last0 : (r == 1 ? lo : hi);
+      }
+      o[b] = v;
     }
-    o[b] = v;
   }
   return total;
 }
 
 // Encode one chunk x[0..n), 17 <= n <= 65536, held in LDS.  `tab` is the
-// u16 hash table, `lid` a u8 scratch of 2048 entries.  Writes to o, returns
-// bytes written.  Mirrors snappy.c:104-195 step for step.
+// u16 hash table, `lid`/`lid2` u8 scratch of 2048 entries each.  Writes to o,
+// returns bytes written.  Mirrors snappy.c:104-195 step for step.
+//
+// Literal-search batches.  Probe index pi = 63 - lane (lane 63 takes the
+// earliest probe).  Each valid probe scatters pi into lid[hash]; the LDS
+// keeps one writer per address (on gfx950 the highest lane, i.e. the
+// earliest probe -- but nothing below depends on which).  A probe that reads
+// back another pi ("loser") shares its hash with another probe of the
+// batch.  Losers then scatter into lid2 the same way, which singles out the
+// second member of each hash group.  When every loser sees its group's
+// winners before itself (checked with two ballots), the winner is the
+// earliest probe of the group and:
+//   * a group's first probe takes its candidate from the table,
+//   * its second probe takes the first probe's position (the serial loop
+//     would have just written it), and
+//   * the batch is cut before the first third member of any group.
+// Otherwise the batch is cut before the earliest loser (lanes before it
+// share no hash with an earlier lane; the first lane never does).  Among the
+// committed probes each group's latest member writes the table.
 __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, uint8_t* lid,
-                                 uint8_t* o) {
+                                 uint8_t* lid2, gptr<uint8_t> o, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
+  const uint32_t pi = 63 - lane;                      // probe index in the batch
   const uint32_t last = n - kMargin;                  // snappy.c:106
 
   uint32_t tsize = 256, shift = 24;                   // snappy.c:108-125
@@ -104,52 +129,75 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
     // ---- literal search from `at` (snappy.c:133-154), 64 probes a step.
     const uint32_t start = at;
     uint32_t k = 0;
-    bool found = false;
     for (;;) {
-      const uint32_t kk = k + lane;
-      const uint32_t kc = kk < kProbeTab ? kk : kProbeTab - 1;
-      const uint32_t p = start + kProbe.off[kc];
-      const uint32_t pn = start + kProbe.off[kc + 1];
-      const bool valid = kk < kProbeTab && pn <= last;            // snappy.c:143
-      const uint64_t vm = __ballot(valid);
-      const uint32_t nvalid = vm == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~vm);
+      uint32_t o0 = off0, o1 = off1;
+      bool in_tab = true;
+      if (k != 0) {                                   // long search: later schedule
+        const uint32_t kk = k + pi;
+        in_tab = kk < kProbeTab;
+        const uint32_t kc = in_tab ? kk : kProbeTab - 1;
+        o0 = kProbe.off[kc];
+        o1 = kProbe.off[kc + 1];
+      }
+      const uint32_t p = start + o0;
+      const bool valid = in_tab && start + o1 <= last;            // snappy.c:143
+      const uint32_t nvalid = (uint32_t)__builtin_popcountll(__ballot(valid));
+      if (nvalid == 0) goto tail;                                 // first probe past limit
 
       uint32_t h = 0, xv = 0;
       if (valid) {
         xv = lds_ld32(x, p);
         h = hash32(xv, shift);
-        lid[h] = (uint8_t)lane;
+        lid[h] = (uint8_t)pi;
       }
       order();
-      const bool loser = valid && lid[h] != lane;
-      const uint64_t lm = __ballot(loser);
-      const uint32_t first_loser = lm ? (uint32_t)__builtin_ctzll(lm) : 64u;
-      const uint32_t nsafe = first_loser > 1 ? first_loser : 1u;
-      const uint32_t nproc = nsafe < nvalid ? nsafe : nvalid;
-      if (nproc == 0) goto tail;                                  // first probe past limit
+      const uint32_t w1 = valid ? lid[h] : 0xffu;
+      const bool loser = valid && w1 != pi;
+      const uint64_t lmask = __ballot(loser);
+      uint32_t ncut = 64, w2 = 0xffu;
+      bool exact2 = false;                                        // second members resolved
+      if (lmask) {
+        bool disorder = __ballot(loser && w1 > pi) != 0;
+        if (valid) lid2[h] = 0xff;
+        order();
+        if (loser) lid2[h] = (uint8_t)pi;
+        order();
+        w2 = valid ? lid2[h] : 0xffu;
+        disorder = disorder || __ballot(loser && w2 > pi) != 0;
+        if (disorder) {
+          const uint32_t first = (uint32_t)__builtin_clzll(lmask); // earliest loser
+          ncut = first > 1 ? first : 1;
+        } else {
+          const uint64_t third = __ballot(loser && w2 != pi);
+          ncut = third ? (uint32_t)__builtin_clzll(third) : 64u;
+          exact2 = true;
+        }
+      }
+      const uint32_t nproc = ncut < nvalid ? ncut : nvalid;
 
-      const bool act = lane < nproc;
+      const bool act = pi < nproc;
+      const uint32_t pfirst = __shfl(p, 63 - (w1 & 63));          // position of w1's probe
       uint32_t cand = 0;
       bool match = false;
       if (act) {
-        cand = tab[h];                                            // snappy.c:146
+        cand = (exact2 && loser) ? pfirst : tab[h];               // snappy.c:146
         match = xv == lds_ld32(x, cand);                          // snappy.c:152
       }
-      const uint64_t mm = __ballot(act && match);
-      const uint32_t ncommit = mm ? (uint32_t)__builtin_ctzll(mm) + 1 : nproc;
-      if (lane < ncommit) tab[h] = (uint16_t)p;                   // snappy.c:148
+      const uint64_t mm = __ballot(match);
+      const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : nproc;
+      // snappy.c:148; a group's first probe defers to its second if both commit.
+      const bool shadowed = exact2 && !loser && w2 < ncommit;
+      if (pi < ncommit && !shadowed) tab[h] = (uint16_t)p;
       order();
       if (mm) {
-        const uint32_t m = ncommit - 1;
-        at = uni(__shfl(p, m));
-        ref = uni(__shfl(cand, m));
-        found = true;
+        const uint32_t src = 63 - (ncommit - 1);
+        at = uni(__shfl(p, src));
+        ref = uni(__shfl(cand, src));
         break;
       }
-      if (nproc < nsafe) goto tail;                               // next probe past limit
+      if (nproc < ncut) goto tail;                                // next probe past limit
       k += nproc;
     }
-    (void)found;
 
     op += emit_literal(o + op, x, lit, at - lit);                 // snappy.c:156
 
@@ -158,6 +206,7 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       const uint32_t base = at;
       uint32_t r = ref + 4;
       at += 4;
+#pragma clang loop unroll(disable)
       for (;;) {                                                  // snappy.c:163-164
         const uint32_t q = at + lane;
         const bool same = q < n && x[r + lane] == x[q];
@@ -197,8 +246,7 @@ tail:
   return op;
 }
 
-// Work item i: input in[in_off[i] .. + in_len[i]) (<= 64 KiB), output at
-// out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
+// Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
 // its varint32 length (snappy.c:368).  Otherwise hdr[i] is the varint value
 // to prefix, or 0xffffffff for none (a later chunk of a > 64 KiB block).
 template <uint32_t IN_CAP, uint32_t WAVES>
@@ -209,22 +257,24 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
   __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap];
-  __shared__ __attribute__((aligned(16))) uint8_t s_lid[WAVES][kTableCap];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lid[WAVES][2][kTableCap];
 
-  const uint32_t wv = threadIdx.x >> 6;
+  // Per-wave scalars go through v_readfirstlane so hipcc keeps the control
+  // flow on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
+  const uint32_t wv = uni(threadIdx.x >> 6);
   const uint32_t slot = blockIdx.x * WAVES + wv;
   if (slot >= n) return;
-  const uint32_t i = index ? index[slot] : slot;
+  const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
+  // Probe offsets of the first 64 probes of a search, kept in registers.
+  const uint32_t off0 = kProbe.off[63 - lane], off1 = kProbe.off[64 - lane];
 
-  const uint32_t len = in_len[i];
-  uint8_t* o = out + out_off[i];
-  const uint32_t sh = stage_in(&s_in[wv][0], in + in_off[i], len);
-  const uint8_t* x = &s_in[wv][sh];
-  order();
+  const uint32_t len = uni(in_len[i]);
+  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
+  const gptr<uint8_t> o = to_global(out) + uni64(out_off[i]);
 
   // varint32 header, coding.h:140-167.
-  const uint32_t hv = hdr ? hdr[i] : len;
+  const uint32_t hv = uni(hdr ? hdr[i] : len);
   uint32_t op = 0;
   if (hv != 0xffffffffu) {
     const uint32_t hl = hv < (1u << 7) ? 1 : hv < (1u << 14) ? 2 : hv < (1u << 21) ? 3
@@ -237,10 +287,20 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     op = hl;
   }
 
-  if (len >= kMinBlock) {
-    op += encode_chunk(x, len, &s_tab[wv][0], &s_lid[wv][0], o + op);
-  } else if (len > 0) {
-    op += emit_literal(o + op, x, 0, len);                       // snappy.c:379-380
+  // snappy.c:370-381: independent 64 KiB chunks, a short tail as a literal.
+  // (IN_CAP >= min(len, 65536) is guaranteed by the launcher.)
+  for (uint32_t c0 = 0; c0 < len; c0 += kChunk) {
+    const uint32_t clen = len - c0 < kChunk ? len - c0 : kChunk;
+    const uint32_t sh = stage_in(&s_in[wv][0], src + c0, clen);
+    const uint8_t* x = &s_in[wv][sh];
+    order();
+    if (clen >= kMinBlock) {
+      op += encode_chunk(x, clen, &s_tab[wv][0], &s_lid[wv][0][0], &s_lid[wv][1][0], o + op,
+                         off0, off1);
+    } else {
+      op += emit_literal(o + op, x, 0, clen);                   // snappy.c:379-380
+    }
+    order();
   }
   if (lane == 0) out_len[i] = op;
 }
@@ -253,8 +313,8 @@ __global__ __launch_bounds__(256) void concat_kernel(
     const uint64_t* __restrict__ dst_off, uint32_t n) {
   const uint32_t p = blockIdx.x;
   if (p >= n) return;
-  const uint8_t* s = src + src_off[p];
-  uint8_t* d = dst + dst_off[p];
+  const gptr<const uint8_t> s = to_global(src) + src_off[p];
+  const gptr<uint8_t> d = to_global(dst) + dst_off[p];
   const uint32_t len = src_len[p];
   for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) d[j] = s[j];
 }
@@ -272,12 +332,12 @@ constexpr uint32_t kEncCap1 = 16896;
 constexpr uint32_t kEncCap2 = 65536;
 
 // max_in: largest item length in the launch (<= 65536).
+// Blocks longer than 64 KiB are encoded chunk by chunk by their wave.
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
   if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
-  if (max_in <= kEncCap2) return launch_encode_cls<kEncCap2, 1>(a, s);
-  return hipErrorInvalidValue;
+  return launch_encode_cls<kEncCap2, 1>(a, s);
 }
 
 hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,

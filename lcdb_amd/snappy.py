@@ -21,14 +21,14 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _native
-from ._native import LGS_MAX_BATCH_BLOCK, LGS_ST_CORRUPT, LGS_ST_NOSPACE, LGS_ST_OK, check
+from ._native import LGS_ST_CORRUPT, LGS_ST_NOSPACE, LGS_ST_OK, check
 
 _L = _native.lib()
 
 __all__ = [
     "encode_size", "encode", "decode_size", "decode",
     "encode_bound", "encode_batch", "decode_batch", "encode_batch_host", "decode_batch_host",
-    "DeviceBatch", "LGS_ST_OK", "LGS_ST_CORRUPT", "LGS_ST_NOSPACE", "LGS_MAX_BATCH_BLOCK",
+    "DeviceBatch", "LGS_ST_OK", "LGS_ST_CORRUPT", "LGS_ST_NOSPACE",
 ]
 
 
@@ -134,7 +134,7 @@ def _pack(blocks: Sequence[bytes]):
 
 
 def encode_batch_host(blocks: Sequence[bytes]) -> list[bytes]:
-    """Encode a list of blocks (each <= 64 KiB) in one GPU launch."""
+    """Encode a list of blocks in one GPU launch."""
     n = len(blocks)
     if n == 0:
         return []
