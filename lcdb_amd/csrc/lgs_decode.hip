@@ -18,6 +18,9 @@
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 namespace lgs {
 
 // Byte source over the stream in global memory (oversized blocks only).
@@ -263,6 +266,161 @@ __device__ __forceinline__ void flush_out(gptr<uint8_t> dst, const uint8_t* o, u
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lane-per-block decoder (large batches of small blocks).
+//
+// One LANE decodes one whole block, straight from HBM to HBM: the tag walk
+// is per-lane VALU code, so one instruction advances up to 64 blocks (the
+// wave-per-block kernel above is bound by the CU's single scalar unit:
+// ~60 SALU instructions per tag).  Byte moves are 16-byte unaligned
+// loads/stores.  Inside a block, writes may run up to 15 bytes past the
+// current op ("wild" chunks) because later ops overwrite them; they never
+// pass the block's end (the last chunk is written byte-exact).  A copy reads
+// bytes this lane stored earlier (same-work-item program order).
+// Overlapping copies (dist < len) use a byte broadcast for dist == 1 (all of
+// fillseq's) and a byte loop otherwise.
+//
+// Inputs must be readable up to 16 bytes past each compressed block.
+// ---------------------------------------------------------------------------
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+
+__device__ __forceinline__ u32x4 ld16(gptr<const uint8_t> p) {
+  return *(gptr<const u32x4_u>)p;
+}
+__device__ __forceinline__ void st16(gptr<uint8_t> p, u32x4 v) { *(gptr<u32x4_u>)p = v; }
+
+__device__ __forceinline__ uint32_t pick(u32x4 v, uint32_t d) {   // v[d], d < 4
+  return d < 2 ? (d == 0 ? v.x : v.y) : (d == 2 ? v.z : v.w);
+}
+
+// 8 bytes starting at p (>= 5 meaningful), via two aligned dword loads.
+__device__ __forceinline__ uint64_t view8(gptr<const uint8_t> p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const gptr<const uint32_t> w = (gptr<const uint32_t>)(a & ~(uintptr_t)3);
+  const uint64_t v = ((uint64_t)w[1] << 32) | w[0];
+  return v >> ((a & 3u) * 8);
+}
+
+// Store the first `len` bytes of the 16-byte value v at p, byte-exact.
+__device__ __forceinline__ void st_exact(gptr<uint8_t> p, u32x4 v, uint32_t len) {
+#pragma clang loop unroll(disable)
+  for (uint32_t b = 0; b < len; ++b) p[b] = (uint8_t)(pick(v, b >> 2) >> (8 * (b & 3u)));
+}
+
+template <uint32_t LANES>
+__global__ __launch_bounds__(64) void decode_lane_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n) {
+  if (threadIdx.x >= LANES) return;
+  const uint32_t slot = blockIdx.x * LANES + threadIdx.x;
+  if (slot >= n) return;
+  const uint32_t i = index ? index[slot] : slot;
+  const gptr<const uint8_t> src = to_global(in) + in_off[i];
+  const uint32_t slen = in_len[i];
+  const gptr<uint8_t> dst = to_global(out) + out_off[i];
+  const uint32_t cap = out_cap[i];
+
+  uint32_t st = 0, want = 0;
+  do {
+    // varint32 header, coding.h:169-204.
+    const uint64_t h = view8(src);
+    uint32_t hlen = 0;
+    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
+      const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
+      if ((b & 0x80u) == 0) {
+        want |= b << (7 * k);
+        hlen = k + 1;
+        break;
+      }
+      want |= (b & 0x7fu) << (7 * k);
+    }
+    if (hlen == 0 || want > 0x7fffffffu) { st = 0; break; }   // snappy.c:405-409
+    if (want > cap) { st = 2; break; }
+
+    uint32_t pos = hlen, made = 0;
+    uint64_t t = pos < slen ? view8(src + pos) : 0;
+    st = 1;
+    while (pos < slen) {                                        // snappy.c:208
+      const uint32_t tag = (uint32_t)t & 0xffu;
+      const uint32_t kind = tag & 3u;
+      const uint32_t left = slen - pos;
+      const uint32_t b1 = (uint32_t)(t >> 8);                  // bytes 1..4
+      uint32_t len, hl, dist = 0;
+      bool bad;
+      if (kind == 0) {                                          // literal, snappy.c:210-273
+        uint32_t m = tag >> 2;
+        hl = 1;
+        bad = false;
+        if (m >= 60) {
+          const uint32_t extra = m - 59;
+          bad = left - 1 < extra;
+          m = extra == 4 ? b1 : (b1 & ((1u << (8 * extra)) - 1u));
+          hl += extra;
+        }
+        len = m + 1;
+        bad = bad || m >= 0x7fffffffu || len > want - made || len > left - hl;
+      } else {                                                  // snappy.c:276-324
+        if (kind == 1) {
+          len = 4 + ((tag >> 2) & 7u);
+          dist = ((tag & 0xe0u) << 3) | (b1 & 0xffu);
+          hl = 2;
+        } else if (kind == 2) {
+          len = 1 + (tag >> 2);
+          dist = b1 & 0xffffu;
+          hl = 3;
+        } else {
+          len = 1 + (tag >> 2);
+          dist = b1;
+          hl = 5;
+        }
+        bad = left < hl || dist == 0 || dist >= 0x80000000u || made < dist ||
+              len > want - made;
+      }
+      if (bad) { st = 0; break; }
+
+      const uint32_t next = pos + hl + (kind == 0 ? len : 0);
+      const uint64_t tn = next < slen ? view8(src + next) : 0;  // prefetch next tag
+
+      const gptr<uint8_t> d = dst + made;
+      if (kind != 0 && dist < len) {
+        // Overlapping copy: the reference's forward byte loop repeats the
+        // dist-byte pattern (snappy.c:329-330).
+        if (dist == 1) {
+          const uint32_t b = d[-1];
+          const uint32_t w4 = b * 0x01010101u;
+          const u32x4 v = {w4, w4, w4, w4};
+#pragma clang loop unroll(disable)
+          for (uint32_t k = 0; k < len; k += 16) {
+            if (made + k + 16 <= want) st16(d + k, v);
+            else st_exact(d + k, v, len - k < 16 ? len - k : 16);
+          }
+        } else {
+#pragma clang loop unroll(disable)
+          for (uint32_t k = 0; k < len; ++k) d[k] = d[(int32_t)k - (int32_t)dist];
+        }
+      } else {
+        const gptr<const uint8_t> sp = kind == 0 ? src + pos + hl : (gptr<const uint8_t>)(d - dist);
+#pragma clang loop unroll(disable)
+        for (uint32_t k = 0; k < len; k += 16) {
+          const u32x4 v = ld16(sp + k);
+          if (made + k + 16 <= want) st16(d + k, v);
+          else st_exact(d + k, v, len - k < 16 ? len - k : 16);
+        }
+      }
+      made += len;
+      pos = next;
+      t = tn;
+    }
+    if (st == 1 && made != want) st = 0;                       // snappy.c:337
+  } while (0);
+
+  status[i] = (uint8_t)st;
+  out_len[i] = st == 1 ? want : 0;
+}
+
 template <uint32_t OUT_CAP, uint32_t IN_CAP, uint32_t WAVES>
 __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -415,8 +573,28 @@ constexpr uint32_t kDecCap0 = 4608;    // fillseq "4 KiB" blocks (max 4208 B)
 constexpr uint32_t kDecCap1 = 16896;   // 16 KiB class
 constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoot)
 
+// Batches of at least this many blocks go to the lane-per-block kernel
+// (one wave per 64 blocks still fills the chip).
+constexpr uint32_t kLaneMinBlocks = 16384;
+
+template <uint32_t LANES>
+static hipError_t launch_decode_lane(const DecodeArgs& a, hipStream_t s) {
+  const uint32_t grid = (a.n + LANES - 1) / LANES;
+  hipLaunchKernelGGL((decode_lane_kernel<LANES>), dim3(grid), dim3(64), 0, s, a.in, a.in_off,
+                     a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+  return hipGetLastError();
+}
+
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  const char* force = getenv("LGS_DECODE_KERNEL");   // "wave" | "lane64" | "lane32"
+  if (force) {
+    if (!strcmp(force, "lane64")) return launch_decode_lane<64>(a, s);
+    if (!strcmp(force, "lane32")) return launch_decode_lane<32>(a, s);
+    if (!strcmp(force, "lane16")) return launch_decode_lane<16>(a, s);
+  } else if (a.n >= kLaneMinBlocks && max_out <= kDecCap1) {
+    return launch_decode_lane<64>(a, s);
+  }
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 5632, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 19968, 1>(a, s);
   if (max_out <= kDecCap2) return launch_decode_cls<kDecCap2, 76800, 1>(a, s);

@@ -30,26 +30,26 @@ namespace lgs {
 
 __constant__ ProbeTable kProbe = ProbeTable();
 
-// snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o.
+// snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o:
+// header (1-3 bytes) and bytes in one pass, lane j writing output byte j.
 // Returns bytes written.
 __device__ __forceinline__ uint32_t emit_literal(gptr<uint8_t> o, const uint8_t* in,
                                                  uint32_t from, uint32_t len) {
   const uint32_t lane = lane_id();
   const uint32_t m = len - 1;
   const uint32_t hl = m < 60 ? 1u : (m < 256 ? 2u : 3u);
-  if (lane < hl) {
-    uint8_t b;
-    if (lane == 0) b = m < 60 ? (uint8_t)(m << 2) : (m < 256 ? (uint8_t)0xf0 : (uint8_t)0xf4);
-    else if (lane == 1) b = (uint8_t)(m & 0xffu);
-    else b = (uint8_t)(m >> 8);
-    o[lane] = b;
-  }
+  const uint32_t h0 = m < 60 ? (m << 2) : (m < 256 ? 0xf0u : 0xf4u);
+  const uint32_t hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);   // little-endian header
+  const uint32_t total = hl + len;
 #pragma clang loop unroll(disable) vectorize(disable)
-  for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
+  for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
     const uint32_t j = j0 + lane;
-    if (j < len) o[hl + j] = in[from + j];
+    // Unconditional (clamped) LDS read, then a select: no branch around it.
+    const uint32_t lb = in[from + (j >= hl ? j - hl : 0)];
+    const uint32_t v = j < hl ? (hdr >> (8 * j)) : lb;
+    if (j < total) o[j] = (uint8_t)v;
   }
-  return hl + len;
+  return total;
 }
 
 // snappy.c:75-102: 64-byte COPY2 pieces while len >= 68, a 60-byte COPY2 if
@@ -57,14 +57,28 @@ __device__ __forceinline__ uint32_t emit_literal(gptr<uint8_t> o, const uint8_t*
 // writes byte b of the emitted sequence.
 __device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, uint32_t len) {
   const uint32_t lane = lane_id();
-  const uint32_t n64 = len >= 68 ? (len - 68) / 64 + 1 : 0;
+  const uint8_t lo = (uint8_t)(dist & 0xffu), hi = (uint8_t)((dist >> 8) & 0xffu);
+  if (len < 68) {                                   // no 64-byte pieces (almost always)
+    const uint32_t has60 = len > 64 ? 1u : 0u;
+    const uint32_t rest = len - 60 * has60;
+    const bool c1 = rest < 12 && dist < 2048;
+    const uint32_t first = c1 ? (((dist >> 8) << 5) | ((rest - 4) << 2) | 1u)
+                              : (((rest - 1) << 2) | 2u);
+    // bytes: [0xee lo hi] (if has60), then first lo [hi]
+    const uint32_t total = 3 * has60 + (c1 ? 2u : 3u);
+    const uint32_t r = lane - 3 * has60;           // index inside the final piece
+    const uint32_t v = lane < 3 * has60 ? (lane == 0 ? 0xeeu : (lane == 1 ? lo : hi))
+                                        : (r == 0 ? first : (r == 1 ? lo : hi));
+    if (lane < total) o[lane] = (uint8_t)v;
+    return total;
+  }
+  const uint32_t n64 = (len - 68) / 64 + 1;
   uint32_t rest = len - 64 * n64;
   const uint32_t has60 = rest > 64 ? 1u : 0u;
   rest -= 60 * has60;
   const bool c1 = rest < 12 && dist < 2048;
   const uint32_t head = 3 * (n64 + has60);
   const uint32_t total = head + (c1 ? 2u : 3u);
-  const uint8_t lo = (uint8_t)(dist & 0xffu), hi = (uint8_t)((dist >> 8) & 0xffu);
   const uint8_t last0 = c1 ? (uint8_t)(((dist >> 8) << 5) | ((rest - 4) << 2) | 1u)
                            : (uint8_t)(((rest - 1) << 2) | 2u);
 #pragma clang loop unroll(disable) vectorize(disable)
@@ -86,17 +100,23 @@ __device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, ui
   return total;
 }
 
+// Index of the scratch slot every table / lane-id array carries past its
+// 2048 real entries: lanes that must not touch a real entry write there
+// instead of branching around the store (keeps the batch free of exec-mask
+// regions, whose save/branch/restore is scalar work).
+constexpr uint32_t kSink = kTableCap;
+
 // Encode one chunk x[0..n), 17 <= n <= 65536, held in LDS.  `tab` is the
-// u16 hash table, `lid`/`lid2` u8 scratch of 2048 entries each.  Writes to o,
-// returns bytes written.  Mirrors snappy.c:104-195 step for step.
+// u16 hash table, `lid` a u8 lane-id scratch (both with a sink slot).  Writes to
+// o, returns bytes written.  Mirrors snappy.c:104-195 step for step.
 //
 // Literal-search batches.  Probe index pi = 63 - lane (lane 63 takes the
 // earliest probe).  Each valid probe scatters pi into lid[hash]; the LDS
 // keeps one writer per address (on gfx950 the highest lane, i.e. the
 // earliest probe -- but nothing below depends on which).  A probe that reads
 // back another pi ("loser") shares its hash with another probe of the
-// batch.  Losers then scatter into lid2 the same way, which singles out the
-// second member of each hash group.  When every loser sees its group's
+// batch.  Losers then scatter their pi into lid again (winners do not), which
+// singles out the second member of each hash group.  When every loser sees its group's
 // winners before itself (checked with two ballots), the winner is the
 // earliest probe of the group and:
 //   * a group's first probe takes its candidate from the table,
@@ -107,7 +127,7 @@ __device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, ui
 // share no hash with an earlier lane; the first lane never does).  Among the
 // committed probes each group's latest member writes the table.
 __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, uint8_t* lid,
-                                 uint8_t* lid2, gptr<uint8_t> o, uint32_t off0, uint32_t off1) {
+                                 gptr<uint8_t> o, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
   const uint32_t pi = 63 - lane;                      // probe index in the batch
   const uint32_t last = n - kMargin;                  // snappy.c:106
@@ -139,36 +159,34 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
         o0 = kProbe.off[kc];
         o1 = kProbe.off[kc + 1];
       }
-      const uint32_t p = start + o0;
       const bool valid = in_tab && start + o1 <= last;            // snappy.c:143
       const uint32_t nvalid = (uint32_t)__builtin_popcountll(__ballot(valid));
       if (nvalid == 0) goto tail;                                 // first probe past limit
+      const uint32_t p = valid ? start + o0 : 0;
 
-      uint32_t h = 0, xv = 0;
-      if (valid) {
-        xv = lds_ld32(x, p);
-        h = hash32(xv, shift);
-        lid[h] = (uint8_t)pi;
-      }
+      const uint32_t xv = lds_ld32(x, p);
+      const uint32_t hh = valid ? hash32(xv, shift) : kSink;
+      lid[hh] = (uint8_t)pi;
       order();
-      const uint32_t w1 = valid ? lid[h] : 0xffu;
-      const bool loser = valid && w1 != pi;
+      const uint32_t w1 = lid[hh];
+      const bool loser = valid & (w1 != pi);
       const uint64_t lmask = __ballot(loser);
       uint32_t ncut = 64, w2 = 0xffu;
       bool exact2 = false;                                        // second members resolved
       if (lmask) {
-        bool disorder = __ballot(loser && w1 > pi) != 0;
-        if (valid) lid2[h] = 0xff;
+        // Round two reuses lid: only losers write, so a group without a
+        // loser still reads its winner back (w2 == w1).
+        bool disorder = __ballot(loser & (w1 > pi)) != 0;
+        lid[loser ? hh : kSink] = (uint8_t)pi;
         order();
-        if (loser) lid2[h] = (uint8_t)pi;
-        order();
-        w2 = valid ? lid2[h] : 0xffu;
-        disorder = disorder || __ballot(loser && w2 > pi) != 0;
+        const uint32_t r2 = lid[hh];
+        w2 = r2 == w1 ? 0xffu : r2;                              // winners: 2nd member or none
+        disorder = disorder || __ballot(loser & (r2 > pi)) != 0;
         if (disorder) {
           const uint32_t first = (uint32_t)__builtin_clzll(lmask); // earliest loser
           ncut = first > 1 ? first : 1;
         } else {
-          const uint64_t third = __ballot(loser && w2 != pi);
+          const uint64_t third = __ballot(loser & (w2 != pi));
           ncut = third ? (uint32_t)__builtin_clzll(third) : 64u;
           exact2 = true;
         }
@@ -177,17 +195,14 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
 
       const bool act = pi < nproc;
       const uint32_t pfirst = __shfl(p, 63 - (w1 & 63));          // position of w1's probe
-      uint32_t cand = 0;
-      bool match = false;
-      if (act) {
-        cand = (exact2 && loser) ? pfirst : tab[h];               // snappy.c:146
-        match = xv == lds_ld32(x, cand);                          // snappy.c:152
-      }
-      const uint64_t mm = __ballot(match);
+      const uint32_t ct = tab[act ? hh : kSink];                  // snappy.c:146
+      const uint32_t cand = (exact2 && loser) ? pfirst : ct;
+      const uint32_t yv = lds_ld32(x, act ? cand : 0);
+      const uint64_t mm = __ballot(act & (xv == yv));             // snappy.c:152
       const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : nproc;
       // snappy.c:148; a group's first probe defers to its second if both commit.
-      const bool shadowed = exact2 && !loser && w2 < ncommit;
-      if (pi < ncommit && !shadowed) tab[h] = (uint16_t)p;
+      const bool shadowed = exact2 & !loser & (w2 < ncommit);
+      tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
       order();
       if (mm) {
         const uint32_t src = 63 - (ncommit - 1);
@@ -209,7 +224,9 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
 #pragma clang loop unroll(disable)
       for (;;) {                                                  // snappy.c:163-164
         const uint32_t q = at + lane;
-        const bool same = q < n && x[r + lane] == x[q];
+        // Clamped unconditional reads (q < n implies r + lane < n).
+        const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
+        const bool same = (q < n) & (x[ra] == x[qa]);
         const uint64_t diff = __ballot(!same);
         if (diff) {
           at += (uint32_t)__builtin_ctzll(diff);
@@ -224,13 +241,14 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       lit = at;
       if (at >= last) goto tail;                                  // snappy.c:169
 
-      const uint64_t w = uni64(lds_ld64(x, at - 1));              // snappy.c:172
-      if (lane == 0) tab[hash32((uint32_t)w, shift)] = (uint16_t)(at - 1);
+      // snappy.c:172-180; every lane stores the same value to the same slot.
+      const uint64_t w = uni64(lds_ld64(x, at - 1));
+      tab[hash32((uint32_t)w, shift)] = (uint16_t)(at - 1);
       order();
-      const uint32_t cur = hash32((uint32_t)(w >> 8), shift);     // snappy.c:177
+      const uint32_t cur = hash32((uint32_t)(w >> 8), shift);
       ref = uni(tab[cur]);
       order();
-      if (lane == 0) tab[cur] = (uint16_t)at;
+      tab[cur] = (uint16_t)at;
       order();
       // lcdb's 64-bit compare (snappy.c:182): bytes at..at+6 against a
       // zero-extended 4-byte load.
@@ -256,8 +274,8 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
-  __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap];
-  __shared__ __attribute__((aligned(16))) uint8_t s_lid[WAVES][2][kTableCap];
+  __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap + 8];   // + sink
+  __shared__ __attribute__((aligned(16))) uint8_t s_lid[WAVES][kTableCap + 16];      // + sink
 
   // Per-wave scalars go through v_readfirstlane so hipcc keeps the control
   // flow on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
@@ -295,8 +313,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* x = &s_in[wv][sh];
     order();
     if (clen >= kMinBlock) {
-      op += encode_chunk(x, clen, &s_tab[wv][0], &s_lid[wv][0][0], &s_lid[wv][1][0], o + op,
-                         off0, off1);
+      op += encode_chunk(x, clen, &s_tab[wv][0], &s_lid[wv][0], o + op, off0, off1);
     } else {
       op += emit_literal(o + op, x, 0, clen);                   // snappy.c:379-380
     }

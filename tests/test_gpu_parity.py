@@ -195,3 +195,40 @@ def test_random_inputs_vs_oracle(gpu):
     outs = gpu.encode_batch_host(blocks)
     for b, o in zip(blocks, outs):
         assert o == ref.encode(b)
+
+
+@pytest.mark.parametrize("kernel", ["wave", "lane64", "lane32"])
+def test_decode_kernel_variants_golden(gpu, vectors, kernel, monkeypatch):
+    # Every decode kernel (forced through LGS_DECODE_KERNEL) against the
+    # reference's accept/reject bit and output, on every golden stream.
+    monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+    enc = [v for v in vectors if v.kind == 0]
+    res, st = gpu.decode_batch_host([v.b for v in enc], [len(v.a) for v in enc])
+    for v, o, s in zip(enc, res, st):
+        assert s == gpu.LGS_ST_OK and o == v.a, (kernel, v.name)
+    dec = [v for v in vectors if v.kind == 1]
+    caps = [len(v.b) if v.ok else 1 << 17 for v in dec]
+    res, st = gpu.decode_batch_host([v.a for v in dec], caps)
+    for v, o, s in zip(dec, res, st):
+        if v.ok:
+            assert s == gpu.LGS_ST_OK and o == v.b, (kernel, v.name)
+        else:
+            assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
+
+
+def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
+    import torch
+    from lcdb_amd import batch
+    d = digests["C2_fillseq_65536x4KiB"]
+    c = corpus.fillseq(65536)
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    for kernel in ("lane64", "lane32", "wave"):
+        monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+        out = batch.decode_slots(c.len)
+        st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+        batch.decode(comp, out, st)
+        torch.cuda.synchronize()
+        assert int(st.sum().item()) == c.n, kernel
+        assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"]), kernel
