@@ -68,13 +68,13 @@ def main() -> None:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from lcdb_amd import batch, corpus, snappy  # noqa: F401  (loads the HIP library)
+    from lcdb_amd import batch, shard, snappy  # noqa: F401  (loads the HIP library)
 
     baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 
     # ---- workload: this rank's round-robin shard of one fillseq stream ----
     t_gen = time.perf_counter()
-    c = corpus.fillseq(a.blocks, block_size=a.block_size, stride=world, phase=rank)
+    c = shard.fillseq_shard(a.blocks, rank, world, a.block_size)
     t_gen = time.perf_counter() - t_gen
     n = c.n
     raw_bytes = c.raw_bytes
@@ -110,11 +110,7 @@ def main() -> None:
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = shard.max_over_ranks(t1 - t0, dist, dev)
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))

@@ -72,10 +72,17 @@ def build_oracle() -> None:
     _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
 
 
+def build_lcdb_harness() -> None:
+    """lcdb compiled in place + its tests linked to the drop-in (oracle/lcdb.mk);
+    a no-op where /root/reference is absent (prebuilt binaries travel)."""
+    _run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "oracle"), "-f", "lcdb.mk"])
+
+
 def build_all(force: bool = False) -> None:
     build_corpus(force)
     build_oracle()
     build_hip(force)
+    build_lcdb_harness()
 
 
 if __name__ == "__main__":

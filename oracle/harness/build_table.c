@@ -1,0 +1,115 @@
+/*
+ * build_table.c -- BASELINE config 5 harness (test infrastructure).
+ *
+ * Builds one SSTable with lcdb's own table path, unchanged:
+ *   memtable (src/memtable.c) of db_bench fillseq entries
+ *     -> ldb_build_table (src/builder.c:35-121)
+ *        -> ldb_tablegen_* (src/table/table_builder.c) -> snappy_encode
+ *        -> re-open + iterate through the table cache (builder.c:99,
+ *           table_cache.c:151) -> ldb_read_block -> snappy_decode
+ * Linked twice by oracle/lcdb.mk: with lcdb's src/util/snappy.c (CPU
+ * reference) and with liblcdb_gpu_snappy.so (the drop-in).  The two .ldb
+ * files must be byte-identical (tests/test_lcdb_integration.py).
+ *
+ * Entries follow bench/db_bench.c fillseq: keys "%016d" (db_bench.c:253-257),
+ * sequence k + 1, 100-byte values from the db_bench value generator
+ * (seed 301, ratio 0.5; db_bench.c:206-246 via src/util/testutil.c).
+ *
+ * usage: build_table DIR NUM_ENTRIES [BLOCK_SIZE]
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "builder.h"
+#include "dbformat.h"
+#include "memtable.h"
+#include "table_cache.h"
+#include "version_edit.h"
+#include "table/iterator.h"
+#include "util/buffer.h"
+#include "util/comparator.h"
+#include "util/env.h"
+#include "util/options.h"
+#include "util/random.h"
+#include "util/slice.h"
+#include "util/status.h"
+#include "util/testutil.h"
+
+int
+main(int argc, char **argv) {
+  const char *dir;
+  long num, k;
+  ldb_comparator_t icmp;
+  ldb_dbopt_t options;
+  ldb_memtable_t *mem;
+  ldb_tables_t *tables;
+  ldb_filemeta_t meta;
+  ldb_iter_t *iter;
+  ldb_buffer_t ring, piece;
+  ldb_rand_t rnd;
+  size_t pos = 0;
+  int rc;
+
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s DIR NUM_ENTRIES [BLOCK_SIZE]\n", argv[0]);
+    return 2;
+  }
+
+  dir = argv[1];
+  num = atol(argv[2]);
+
+  ldb_ikc_init(&icmp, ldb_bytewise_comparator);
+  options = *ldb_dbopt_default;
+  options.comparator = &icmp;
+  if (argc > 3)
+    options.block_size = (size_t)atol(argv[3]);
+
+  ldb_create_dir(dir);
+
+  /* db_bench value ring: compressible 100-byte pieces, >= 1 MiB. */
+  ldb_buffer_init(&ring);
+  ldb_buffer_init(&piece);
+  ldb_rand_init(&rnd, 301);
+  while (ring.size < 1048576) {
+    ldb_compressible_string(&piece, &rnd, 0.5, 100);
+    ldb_buffer_concat(&ring, &piece);
+  }
+
+  mem = ldb_memtable_create(&icmp);
+  ldb_memtable_ref(mem);
+
+  for (k = 0; k < num; k++) {
+    char kbuf[32];
+    ldb_slice_t key, val;
+
+    sprintf(kbuf, "%016d", (int)k);
+    key = ldb_slice((uint8_t *)kbuf, 16);
+
+    if (pos + 100 > ring.size)
+      pos = 0;
+    val = ldb_slice(ring.data + pos, 100);
+    pos += 100;
+
+    ldb_memtable_add(mem, (ldb_seqnum_t)(k + 1), LDB_TYPE_VALUE, &key, &val);
+  }
+
+  tables = ldb_tables_create(dir, &options, 100);
+
+  ldb_filemeta_init(&meta);
+  meta.number = 1;
+
+  iter = ldb_memiter_create(mem);
+  rc = ldb_build_table(dir, &options, tables, iter, &meta);
+  ldb_iter_destroy(iter);
+
+  printf("rc=%d (%s) file_size=%lu\n", rc, ldb_strerror(rc),
+         (unsigned long)meta.file_size);
+
+  ldb_tables_destroy(tables);
+  ldb_memtable_unref(mem);
+  ldb_buffer_clear(&piece);
+  ldb_buffer_clear(&ring);
+
+  return rc == LDB_OK ? 0 : 1;
+}

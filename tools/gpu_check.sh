@@ -23,7 +23,7 @@ run() {   # name limit cmd...
 for s in $steps; do
   case $s in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
-    alltests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    alltests) run pytest_gpu 1100 python -m pytest tests -m gpu -q -p no:cacheprovider --durations=15 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
