@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""PCIe-inclusive rate of the codec on BASELINE config 2 (recorded in DESIGN.md,
+never bench.py's `value`).
+
+Host side: the corpus in pinned host memory (as the .ldb reader/builder would
+stage it).  One encode pass = H2D raw blocks + encode + D2H encoded slots;
+one decode pass = H2D encoded slots + decode + D2H raw blocks; hipMemcpyAsync
+on the codec's stream, timed with events, median over --steps.  Encoded slots
+are bound-spaced (the D2H moves slot capacity, an upper bound on a compacted
+transfer); the packed-compressed-bytes figure is reported beside it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from lcdb_amd import batch, corpus  # noqa: E402
+
+
+def main() -> None:
+    p = argparse.ArgumentParser()
+    p.add_argument("--blocks", type=int, default=65536)
+    p.add_argument("--steps", type=int, default=10)
+    a = p.parse_args()
+    c = corpus.fillseq(a.blocks)
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    out = batch.decode_slots(c.len)
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    h_raw = torch.from_numpy(c.buf).pin_memory()
+    h_comp = torch.empty(comp.buf.numel(), dtype=torch.uint8).pin_memory()
+    h_out = torch.empty(out.buf.numel(), dtype=torch.uint8).pin_memory()
+    s = torch.cuda.current_stream()
+    batch.encode(raw, comp)
+    torch.cuda.synchronize()
+    comp_bytes = int(comp.len.sum().item())
+
+    def timed(fn):
+        ts = []
+        for _ in range(a.steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            fn()
+            e1.record(s)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        return float(np.median(ts))
+
+    def enc_pass():
+        raw.buf.copy_(h_raw, non_blocking=True)
+        batch.encode(raw, comp)
+        h_comp.copy_(comp.buf, non_blocking=True)
+
+    def dec_pass():
+        comp.buf.copy_(h_comp, non_blocking=True)
+        batch.decode(comp, out, st)
+        h_out.copy_(out.buf, non_blocking=True)
+
+    def h2d_raw():
+        raw.buf.copy_(h_raw, non_blocking=True)
+
+    te, td, th = timed(enc_pass), timed(dec_pass), timed(h2d_raw)
+    assert bool((st == 1).all())
+    rb = c.raw_bytes
+    print(json.dumps({
+        "blocks": c.n, "raw_bytes": rb, "comp_bytes_packed": comp_bytes,
+        "comp_slot_bytes": comp.buf.numel(), "h2d_raw_GBps": h_raw.numel() / th / 1e9,
+        "encode_pcie_GiBps": rb / te / 2**30, "decode_pcie_GiBps": rb / td / 2**30,
+        "roundtrip_pcie_GiBps": rb / (te + td) / 2**30,
+        "encode_pass_ms": te * 1e3, "decode_pass_ms": td * 1e3}))
+
+
+if __name__ == "__main__":
+    main()
