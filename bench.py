@@ -51,6 +51,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--cpu-sample", type=int, default=16384, help="blocks in the CPU sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--no-pipelined", action="store_true",
+                   help="skip the extra concurrent encode||decode measurement")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                    help="PMC traffic summary (written by tools/profile_traffic.py)")
     return p.parse_args()
@@ -111,6 +113,36 @@ def main() -> None:
     if dist:
         dist.barrier()
     elapsed = shard.max_over_ranks(t1 - t0, dist, dev)
+
+    # ---- extra (not `value`): encode and decode concurrently on two streams,
+    # step k encoding copy k while decoding what step k-1 encoded -- the shape
+    # of a store that compacts (writes) while serving reads.
+    pipelined = None
+    if not a.no_pipelined and a.copies >= 2:
+        s_enc, s_dec = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        enc_done = [torch.cuda.Event() for _ in range(a.copies)]
+        dec_done = [torch.cuda.Event() for _ in range(a.copies)]
+        batch.encode(raws[0], comps[0], s_enc)
+        enc_done[0].record(s_enc)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t0p = time.perf_counter()
+        for k in range(1, a.steps + 1):
+            j, jp = k % a.copies, (k - 1) % a.copies
+            if k >= a.copies:
+                s_enc.wait_event(dec_done[j])        # the decode reading slot j is done
+            batch.encode(raws[j], comps[j], s_enc)
+            enc_done[j].record(s_enc)
+            s_dec.wait_event(enc_done[jp])           # decode what step k-1 encoded
+            batch.decode(comps[jp], outs[jp], stats[jp], s_dec)
+            dec_done[jp].record(s_dec)
+        torch.cuda.synchronize()
+        tp = shard.max_over_ranks(time.perf_counter() - t0p, dist, dev)
+        pipelined = {"GiBps": raw_bytes * world * a.steps / tp / 2**30,
+                     "ms_per_step": tp / a.steps * 1e3,
+                     "note": "encode(step k) || decode(step k-1) on two streams; extra field, "
+                             "not value"}
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
@@ -175,6 +207,7 @@ def main() -> None:
             "encode_GiBps": raw_bytes * world / (enc_ms * 1e-3) / 2**30,
             "decode_GiBps": raw_bytes * world / (dec_ms * 1e-3) / 2**30,
             "kernels": kern, "roofline": roof, "cpu_baseline": cpu, "parity": parity,
+            "pipelined": pipelined,
             "gen_seconds": t_gen,
         }
         print(json.dumps(line), flush=True)

@@ -26,14 +26,28 @@
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 namespace lgs {
 
 __constant__ ProbeTable kProbe = ProbeTable();
 
+// Output slot of one block as a raw buffer: byte offset = SGPR cursor +
+// VGPR lane offset, so stores need no 64-bit address arithmetic, and the
+// hardware range check (num_records = the encode bound) keeps every store
+// inside the slot.
+struct OutSlot {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ void put(uint32_t soff, uint32_t voff, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)voff, (int)soff, 0);
+  }
+};
+
 // snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o:
 // header (1-3 bytes) and bytes in one pass, lane j writing output byte j.
 // Returns bytes written.
-__device__ __forceinline__ uint32_t emit_literal(gptr<uint8_t> o, const uint8_t* in,
+__device__ __forceinline__ uint32_t emit_literal(const OutSlot& o, uint32_t op, const uint8_t* in,
                                                  uint32_t from, uint32_t len) {
   const uint32_t lane = lane_id();
   const uint32_t m = len - 1;
@@ -47,7 +61,7 @@ __device__ __forceinline__ uint32_t emit_literal(gptr<uint8_t> o, const uint8_t*
     // Unconditional (clamped) LDS read, then a select: no branch around it.
     const uint32_t lb = in[from + (j >= hl ? j - hl : 0)];
     const uint32_t v = j < hl ? (hdr >> (8 * j)) : lb;
-    if (j < total) o[j] = (uint8_t)v;
+    if (j < total) o.put(op, j, v);
   }
   return total;
 }
@@ -55,7 +69,8 @@ __device__ __forceinline__ uint32_t emit_literal(gptr<uint8_t> o, const uint8_t*
 // snappy.c:75-102: 64-byte COPY2 pieces while len >= 68, a 60-byte COPY2 if
 // then len > 64, then COPY2 (len >= 12 or dist >= 2048) or COPY1.  Lane b
 // writes byte b of the emitted sequence.
-__device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, uint32_t len) {
+__device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uint32_t dist,
+                                              uint32_t len) {
   const uint32_t lane = lane_id();
   const uint8_t lo = (uint8_t)(dist & 0xffu), hi = (uint8_t)((dist >> 8) & 0xffu);
   if (len < 68) {                                   // no 64-byte pieces (almost always)
@@ -69,7 +84,7 @@ __device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, ui
     const uint32_t r = lane - 3 * has60;           // index inside the final piece
     const uint32_t v = lane < 3 * has60 ? (lane == 0 ? 0xeeu : (lane == 1 ? lo : hi))
                                         : (r == 0 ? first : (r == 1 ? lo : hi));
-    if (lane < total) o[lane] = (uint8_t)v;
+    if (lane < total) o.put(op, lane, v);
     return total;
   }
   const uint32_t n64 = (len - 68) / 64 + 1;
@@ -94,7 +109,7 @@ __device__ __forceinline__ uint32_t emit_copy(gptr<uint8_t> o, uint32_t dist, ui
         const uint32_t r = b - head;
         v = r == 0 ? last0 : (r == 1 ? lo : hi);
       }
-      o[b] = v;
+      o.put(op, b, v);
     }
   }
   return total;
@@ -127,7 +142,7 @@ constexpr uint32_t kSink = kTableCap;
 // share no hash with an earlier lane; the first lane never does).  Among the
 // committed probes each group's latest member writes the table.
 __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, uint8_t* lid,
-                                 gptr<uint8_t> o, uint32_t off0, uint32_t off1) {
+                                 const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
   const uint32_t pi = 63 - lane;                      // probe index in the batch
   const uint32_t last = n - kMargin;                  // snappy.c:106
@@ -140,7 +155,7 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
   for (uint32_t e = lane; e < tsize; e += kWave) tab[e] = 0;   // snappy.c:129
   order();
 
-  uint32_t op = 0;       // output cursor
+  uint32_t op = op0;     // output cursor (byte offset in the slot)
   uint32_t lit = 0;      // first byte not yet emitted (snappy.c:111 "emit")
   uint32_t at = 1;       // snappy.c:112
   uint32_t ref = 0;
@@ -166,6 +181,10 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
 
       const uint32_t xv = lds_ld32(x, p);
       const uint32_t hh = valid ? hash32(xv, shift) : kSink;
+      // The table read and the candidate's bytes do not depend on the
+      // lane-id rounds below: issue them first so their LDS latency overlaps.
+      const uint32_t ct = tab[hh];                                // snappy.c:146
+      const uint32_t yt = lds_ld32(x, valid ? ct : 0);
       lid[hh] = (uint8_t)pi;
       order();
       const uint32_t w1 = lid[hh];
@@ -194,10 +213,14 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       const uint32_t nproc = ncut < nvalid ? ncut : nvalid;
 
       const bool act = pi < nproc;
-      const uint32_t pfirst = __shfl(p, 63 - (w1 & 63));          // position of w1's probe
-      const uint32_t ct = tab[act ? hh : kSink];                  // snappy.c:146
-      const uint32_t cand = (exact2 && loser) ? pfirst : ct;
-      const uint32_t yv = lds_ld32(x, act ? cand : 0);
+      // A group's second probe compares against the first probe's bytes,
+      // which that lane already holds.
+      const uint32_t src1 = 63 - (w1 & 63);
+      const uint32_t pfirst = __shfl(p, src1);                    // position of w1's probe
+      const uint32_t xfirst = __shfl(xv, src1);
+      const bool use_first = exact2 & loser;
+      const uint32_t cand = use_first ? pfirst : ct;
+      const uint32_t yv = use_first ? xfirst : yt;
       const uint64_t mm = __ballot(act & (xv == yv));             // snappy.c:152
       const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : nproc;
       // snappy.c:148; a group's first probe defers to its second if both commit.
@@ -214,7 +237,7 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       k += nproc;
     }
 
-    op += emit_literal(o + op, x, lit, at - lit);                 // snappy.c:156
+    op += emit_literal(o, op, x, lit, at - lit);                  // snappy.c:156
 
     // ---- copies, with lcdb's immediate re-match (snappy.c:158-187).
     for (;;) {
@@ -237,7 +260,7 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       }
       at = uni(at);
 
-      op += emit_copy(o + op, base - ref, at - base);             // snappy.c:166
+      op += emit_copy(o, op, base - ref, at - base);              // snappy.c:166
       lit = at;
       if (at >= last) goto tail;                                  // snappy.c:169
 
@@ -260,7 +283,7 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
   }
 
 tail:
-  if (lit < n) op += emit_literal(o + op, x, lit, n - lit);        // snappy.c:190-192
+  if (lit < n) op += emit_literal(o, op, x, lit, n - lit);         // snappy.c:190-192
   return op;
 }
 
@@ -289,7 +312,8 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
 
   const uint32_t len = uni(in_len[i]);
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
-  const gptr<uint8_t> o = to_global(out) + uni64(out_off[i]);
+  const OutSlot o{__builtin_amdgcn_make_buffer_rsrc(out + uni64(out_off[i]), 0,
+                                                    (int)(32 + len + len / 6), 0x00020000)};
 
   // varint32 header, coding.h:140-167.
   const uint32_t hv = uni(hdr ? hdr[i] : len);
@@ -300,7 +324,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     if (lane < hl) {
       uint32_t b = (hv >> (7 * lane)) & 0x7fu;
       if (lane + 1 < hl) b |= 0x80u;
-      o[lane] = (uint8_t)b;
+      o.put(0, lane, b);
     }
     op = hl;
   }
@@ -313,9 +337,9 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* x = &s_in[wv][sh];
     order();
     if (clen >= kMinBlock) {
-      op += encode_chunk(x, clen, &s_tab[wv][0], &s_lid[wv][0], o + op, off0, off1);
+      op = encode_chunk(x, clen, &s_tab[wv][0], &s_lid[wv][0], o, op, off0, off1);
     } else {
-      op += emit_literal(o + op, x, 0, clen);                   // snappy.c:379-380
+      op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
     order();
   }
@@ -350,8 +374,14 @@ constexpr uint32_t kEncCap2 = 65536;
 
 // max_in: largest item length in the launch (<= 65536).
 // Blocks longer than 64 KiB are encoded chunk by chunk by their wave.
+// LGS_ENCODE_KERNEL=wave|group16|group32|group64 forces a variant (A/B).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  const char* force = getenv("LGS_ENCODE_KERNEL");
+  if (force && !strncmp(force, "group", 5)) {
+    const hipError_t e = launch_encode_group(a, max_in, (uint32_t)atoi(force + 5), s);
+    if (e != hipErrorNotSupported) return e;
+  }
   if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
   if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
   return launch_encode_cls<kEncCap2, 1>(a, s);

@@ -23,6 +23,10 @@ struct EncodeArgs {
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
 // max_in: largest item length in the launch (<= 65536).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s);
+// Several-blocks-per-wave encoder (lgs_encode_group.hip); lanes per block =
+// 16, 32 or 64.  hipErrorNotSupported if the batch does not qualify.
+hipError_t launch_encode_group(const EncodeArgs& a, uint32_t max_in, uint32_t lanes,
+                               hipStream_t s);
 hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                          uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s);
 

@@ -232,3 +232,25 @@ def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
         torch.cuda.synchronize()
         assert int(st.sum().item()) == c.n, kernel
         assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"]), kernel
+
+
+@pytest.mark.parametrize("kernel", ["wave", "group64", "group32", "group16"])
+def test_encode_kernel_variants(gpu, vectors, digests, kernel, monkeypatch):
+    # Every encode kernel (forced through LGS_ENCODE_KERNEL) against the
+    # reference's bytes: all golden inputs in one batch (the group kernels
+    # take batches of blocks <= 4608 B; larger batches fall back), then the
+    # full C1 corpus on the device.
+    monkeypatch.setenv("LGS_ENCODE_KERNEL", kernel)
+    small = [v for v in vectors if v.kind == 0 and len(v.a) <= 4608]
+    outs = gpu.encode_batch_host([v.a for v in small])
+    for v, o in zip(small, outs):
+        assert o == v.b, (kernel, v.name)
+    import torch
+    from lcdb_amd import batch
+    d = digests["C1_fillseq_1024x4KiB"]
+    c = corpus.fillseq(1024)
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    torch.cuda.synchronize()
+    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"]), kernel
