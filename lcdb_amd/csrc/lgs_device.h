@@ -64,6 +64,24 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Moves a wave-uniform value into a VGPR and hides that it is uniform, so
+// arithmetic on the result is issued on the VALU.  A CU has one scalar unit
+// for its four SIMDs but twice the scalar unit's instruction rate in VALU
+// issue, and the encoder's per-copy bookkeeping otherwise lands on the SALU.
+__device__ __forceinline__ uint32_t vec(uint32_t v) {
+  asm("" : "+v"(v));
+  return v;
+}
+
+// Wave ballot as a plain compare into an SGPR pair (HIP's __ballot adds a
+// v_cndmask/v_cmp round trip).
+__device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+// Value of v in lane l (l wave-uniform): v_readlane, no LDS round trip.
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, uint32_t l) {
+  return __builtin_amdgcn_readlane(v, l);
+}
+
 // snappy.c:44-47 (argument truncated to 32 bits at every call site).
 __device__ __forceinline__ uint32_t hash32(uint32_t v, uint32_t shift) {
   return (v * kHashMul) >> shift;

@@ -115,6 +115,65 @@ __device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uin
   return total;
 }
 
+// snappy.c:53-102, the common case in one pass: the pending literal
+// x[lit .. lit+L) (L == 0: none) followed by a copy of length C < 68 at
+// distance D (C == 0: none).  Lane b writes byte b of the sequence.  The
+// header and tag arithmetic runs on the VALU (vec()), selects replace
+// branches, and lanes past the end store at an out-of-range offset that the
+// buffer range check drops, so the pass has no exec-mask regions (their
+// save/restore is scalar work, and the scalar unit is what this kernel
+// saturates).  Returns bytes written.
+__device__ __forceinline__ uint32_t emit_seq(const OutSlot& o, uint32_t op, const uint8_t* x,
+                                             uint32_t n, uint32_t lit, uint32_t L, uint32_t D,
+                                             uint32_t C) {
+  // Every ?: below picks between values already computed: clang lowers a
+  // conditional whose arms still hold work to branches (exec-mask regions).
+  const uint32_t lane = lane_id();
+  const uint32_t vL = vec(L), vD = vec(D), vC = vec(C), vlit = vec(lit);
+  const uint32_t m = vL - 1;                                          // snappy.c:55-66
+  const uint32_t hl_big = m < 256 ? 2u : 3u;
+  const uint32_t hl_any = m < 60 ? 1u : hl_big;
+  const uint32_t hl = vL == 0 ? 0u : hl_any;
+  const uint32_t h0_big = m < 256 ? 0xf0u : 0xf4u;
+  const uint32_t m4 = m << 2;
+  const uint32_t h0 = m < 60 ? m4 : h0_big;
+  const uint32_t hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);
+  const uint32_t has60 = vC > 64 ? 3u : 0u;                           // snappy.c:84-89
+  const uint32_t rest = vC - 20 * has60;
+  // rest < 12 && D < 2048 (snappy.c:91), as sign bits: no lane-mask logic.
+  const bool c1 = (int32_t)((rest - 12) & (vD - 2048)) < 0;
+  const uint32_t f1 = ((vD >> 8) << 5) | ((rest - 4) << 2) | 1u;      // snappy.c:98
+  const uint32_t f2 = ((rest - 1) << 2) | 2u;                         // snappy.c:92
+  const uint32_t first = c1 ? f1 : f2;
+  const uint32_t ntag = c1 ? 2u : 3u;
+  const uint32_t ctag = has60 + ntag;
+  const uint32_t ctot = vC == 0 ? 0u : ctag;
+  const uint32_t lend = hl + vL;                                      // first copy byte
+  const uint32_t vtotal = lend + ctot;
+  const uint32_t dlo = vD, dhi = vD >> 8;
+  const uint32_t total = uni(vtotal);
+#pragma clang loop unroll(disable) vectorize(disable)
+  for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
+    const uint32_t b = vec(j0) + lane;
+    const uint32_t ia = vlit + b - hl;                                // underflows for b < hl
+    const uint32_t iac = ia < n ? ia : n;
+    const uint32_t lb = x[iac];
+    const uint32_t cb = b - lend;                                     // byte of the copy tags
+    const uint32_t r = cb - has60;
+    const uint32_t t60 = cb == 1 ? dlo : dhi;
+    const uint32_t p60 = cb == 0 ? 0xeeu : t60;                       // the 60-byte piece
+    const uint32_t tr = r == 1 ? dlo : dhi;
+    const uint32_t pr = r == 0 ? first : tr;                          // the final piece
+    const uint32_t cv = cb < has60 ? p60 : pr;
+    const uint32_t hb = hdr >> ((8 * b) & 31);
+    const uint32_t bv = b < lend ? lb : cv;
+    const uint32_t v = b < hl ? hb : bv;
+    const uint32_t voff = b < vtotal ? b : 0x40000000u;               // dropped by the range check
+    o.put(op, voff, v);
+  }
+  return total;
+}
+
 // Index of the scratch slot every table / lane-id array carries past its
 // 2048 real entries: lanes that must not touch a real entry write there
 // instead of branching around the store (keeps the batch free of exec-mask
@@ -132,7 +191,7 @@ constexpr uint32_t kSink = kTableCap;
 // back another pi ("loser") shares its hash with another probe of the
 // batch.  Losers then scatter their pi into lid again (winners do not), which
 // singles out the second member of each hash group.  When every loser sees its group's
-// winners before itself (checked with two ballots), the winner is the
+// winners before itself (checked with a ballot), the winner is the
 // earliest probe of the group and:
 //   * a group's first probe takes its candidate from the table,
 //   * its second probe takes the first probe's position (the serial loop
@@ -141,6 +200,10 @@ constexpr uint32_t kSink = kTableCap;
 // Otherwise the batch is cut before the earliest loser (lanes before it
 // share no hash with an earlier lane; the first lane never does).  Among the
 // committed probes each group's latest member writes the table.
+//
+// A found match is extended, then its literal and copy are emitted in one
+// pass (emit_seq), then lcdb's immediate re-probe runs (snappy.c:172-186)
+// as identical work on every lane.
 __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, uint8_t* lid,
                                  const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
@@ -175,8 +238,8 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
         o1 = kProbe.off[kc + 1];
       }
       const bool valid = in_tab && start + o1 <= last;            // snappy.c:143
-      const uint32_t nvalid = (uint32_t)__builtin_popcountll(__ballot(valid));
-      if (nvalid == 0) goto tail;                                 // first probe past limit
+      const uint64_t vmask = ballot(valid);
+      if (vmask == 0) goto tail;                                  // first probe past limit
       const uint32_t p = valid ? start + o0 : 0;
 
       const uint32_t xv = lds_ld32(x, p);
@@ -184,60 +247,51 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       // The table read and the candidate's bytes do not depend on the
       // lane-id rounds below: issue them first so their LDS latency overlaps.
       const uint32_t ct = tab[hh];                                // snappy.c:146
-      const uint32_t yt = lds_ld32(x, valid ? ct : 0);
+      uint32_t yv = lds_ld32(x, valid ? ct : 0);
       lid[hh] = (uint8_t)pi;
       order();
       const uint32_t w1 = lid[hh];
       const bool loser = valid & (w1 != pi);
-      const uint64_t lmask = __ballot(loser);
+      const uint64_t lmask = ballot(loser);
       uint32_t ncut = 64, w2 = 0xffu;
-      bool exact2 = false;                                        // second members resolved
+      uint64_t second = 0;                                        // lanes comparing to their group's first
       if (lmask) {
         // Round two reuses lid: only losers write, so a group without a
         // loser still reads its winner back (w2 == w1).
-        bool disorder = __ballot(loser & (w1 > pi)) != 0;
         lid[loser ? hh : kSink] = (uint8_t)pi;
         order();
         const uint32_t r2 = lid[hh];
         w2 = r2 == w1 ? 0xffu : r2;                              // winners: 2nd member or none
-        disorder = disorder || __ballot(loser & (r2 > pi)) != 0;
-        if (disorder) {
+        const uint32_t wmax = w1 > r2 ? w1 : r2;
+        if (ballot(loser & (wmax > pi))) {                        // a group out of order
           const uint32_t first = (uint32_t)__builtin_clzll(lmask); // earliest loser
           ncut = first > 1 ? first : 1;
         } else {
-          const uint64_t third = __ballot(loser & (w2 != pi));
+          const uint64_t third = ballot(loser & (w2 != pi));
           ncut = third ? (uint32_t)__builtin_clzll(third) : 64u;
-          exact2 = true;
+          second = lmask;
+          // A group's second probe compares against the first probe's
+          // bytes, which that lane already holds.
+          const uint32_t xfirst = __shfl(xv, 63 - (w1 & 63));
+          yv = loser ? xfirst : yv;
         }
       }
-      const uint32_t nproc = ncut < nvalid ? ncut : nvalid;
-
-      const bool act = pi < nproc;
-      // A group's second probe compares against the first probe's bytes,
-      // which that lane already holds.
-      const uint32_t src1 = 63 - (w1 & 63);
-      const uint32_t pfirst = __shfl(p, src1);                    // position of w1's probe
-      const uint32_t xfirst = __shfl(xv, src1);
-      const bool use_first = exact2 & loser;
-      const uint32_t cand = use_first ? pfirst : ct;
-      const uint32_t yv = use_first ? xfirst : yt;
-      const uint64_t mm = __ballot(act & (xv == yv));             // snappy.c:152
-      const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : nproc;
+      const uint64_t mm = ballot((pi < ncut) & (xv == yv)) & vmask;   // snappy.c:152
+      const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
       // snappy.c:148; a group's first probe defers to its second if both commit.
-      const bool shadowed = exact2 & !loser & (w2 < ncommit);
+      const bool shadowed = (second != 0) & !loser & (w2 < ncommit);
       tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
       order();
       if (mm) {
         const uint32_t src = 63 - (ncommit - 1);
-        at = uni(__shfl(p, src));
-        ref = uni(__shfl(cand, src));
+        at = lane_val(p, src);
+        ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
+                                    : lane_val(ct, src);
         break;
       }
-      if (nproc < ncut) goto tail;                                // next probe past limit
-      k += nproc;
+      if ((uint32_t)__builtin_popcountll(vmask) < ncut) goto tail; // next probe past limit
+      k += ncut;
     }
-
-    op += emit_literal(o, op, x, lit, at - lit);                  // snappy.c:156
 
     // ---- copies, with lcdb's immediate re-match (snappy.c:158-187).
     for (;;) {
@@ -250,7 +304,7 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
         // Clamped unconditional reads (q < n implies r + lane < n).
         const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
         const bool same = (q < n) & (x[ra] == x[qa]);
-        const uint64_t diff = __ballot(!same);
+        const uint64_t diff = ballot(!same);
         if (diff) {
           at += (uint32_t)__builtin_ctzll(diff);
           break;
@@ -258,27 +312,35 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
         at += kWave;
         r += kWave;
       }
-      at = uni(at);
 
-      op += emit_copy(o, op, base - ref, at - base);              // snappy.c:166
+      // snappy.c:156 + 166: the literal before the copy, then the copy.
+      const uint32_t clen = at - base, dist = base - ref;
+      if (clen < 68) {
+        op += emit_seq(o, op, x, n, lit, base - lit, dist, clen);
+      } else {
+        op += emit_seq(o, op, x, n, lit, base - lit, 0, 0);
+        op += emit_copy(o, op, dist, clen);
+      }
       lit = at;
       if (at >= last) goto tail;                                  // snappy.c:169
 
-      // snappy.c:172-180; every lane stores the same value to the same slot.
-      const uint64_t w = uni64(lds_ld64(x, at - 1));
-      tab[hash32((uint32_t)w, shift)] = (uint16_t)(at - 1);
+      // snappy.c:172-180, as identical work on every lane (VALU + LDS
+      // broadcast).  lcdb's 64-bit compare (snappy.c:182): bytes at..at+6
+      // against a zero-extended 4-byte load.
+      const uint32_t va = vec(at);
+      const uint64_t w = lds_ld64(x, va - 1);
+      const uint32_t h1 = hash32((uint32_t)w, shift), h2 = hash32((uint32_t)(w >> 8), shift);
+      tab[h1] = (uint16_t)(va - 1);
       order();
-      const uint32_t cur = hash32((uint32_t)(w >> 8), shift);
-      ref = uni(tab[cur]);
+      const uint32_t c = tab[h2];
       order();
-      tab[cur] = (uint16_t)at;
+      tab[h2] = (uint16_t)va;
       order();
-      // lcdb's 64-bit compare (snappy.c:182): bytes at..at+6 against a
-      // zero-extended 4-byte load.
-      if ((w >> 8) != (uint64_t)uni(lds_ld32(x, ref))) {
+      if (ballot((w >> 8) != (uint64_t)lds_ld32(x, c))) {
         ++at;
         break;
       }
+      ref = uni(c);
     }
   }
 
