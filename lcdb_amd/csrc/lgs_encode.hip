@@ -220,128 +220,133 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
 
   uint32_t op = op0;     // output cursor (byte offset in the slot)
   uint32_t lit = 0;      // first byte not yet emitted (snappy.c:111 "emit")
-  uint32_t at = 1;       // snappy.c:112
-  uint32_t ref = 0;
+  uint32_t start = 1;    // where the current literal search began (snappy.c:112)
+  uint32_t k = 0;        // probes of this search already done
 
+  // One loop with one exit: each trip is one 64-probe batch of a literal
+  // search and, when the batch finds a match, the copies that follow it.
+  // (Loops with several exits get a selector variable and compare chains
+  // from the compiler's loop-exit unification: scalar work on every trip.)
   for (;;) {
-    // ---- literal search from `at` (snappy.c:133-154), 64 probes a step.
-    const uint32_t start = at;
-    uint32_t k = 0;
-    for (;;) {
-      uint32_t o0 = off0, o1 = off1;
-      bool in_tab = true;
-      if (k != 0) {                                   // long search: later schedule
-        const uint32_t kk = k + pi;
-        in_tab = kk < kProbeTab;
-        const uint32_t kc = in_tab ? kk : kProbeTab - 1;
-        o0 = kProbe.off[kc];
-        o1 = kProbe.off[kc + 1];
-      }
-      const bool valid = in_tab && start + o1 <= last;            // snappy.c:143
-      const uint64_t vmask = ballot(valid);
-      if (vmask == 0) goto tail;                                  // first probe past limit
-      const uint32_t p = valid ? start + o0 : 0;
+    // ---- literal search (snappy.c:133-154), probes k .. k+63 of the search.
+    uint32_t o0 = off0, o1 = off1;
+    bool in_tab = true;
+    if (k != 0) {                                   // long search: later schedule
+      const uint32_t kk = k + pi;
+      in_tab = kk < kProbeTab;
+      const uint32_t kc = in_tab ? kk : kProbeTab - 1;
+      o0 = kProbe.off[kc];
+      o1 = kProbe.off[kc + 1];
+    }
+    const bool valid = in_tab && start + o1 <= last;              // snappy.c:143
+    const uint64_t vmask = ballot(valid);
+    const uint32_t p = valid ? start + o0 : 0;
 
-      const uint32_t xv = lds_ld32(x, p);
-      const uint32_t hh = valid ? hash32(xv, shift) : kSink;
-      // The table read and the candidate's bytes do not depend on the
-      // lane-id rounds below: issue them first so their LDS latency overlaps.
-      const uint32_t ct = tab[hh];                                // snappy.c:146
-      uint32_t yv = lds_ld32(x, valid ? ct : 0);
-      lid[hh] = (uint8_t)pi;
+    const uint32_t xv = lds_ld32(x, p);
+    const uint32_t hh = valid ? hash32(xv, shift) : kSink;
+    // The table read and the candidate's bytes do not depend on the
+    // lane-id rounds below: issue them first so their LDS latency overlaps.
+    const uint32_t ct = tab[hh];                                  // snappy.c:146
+    uint32_t yv = lds_ld32(x, valid ? ct : 0);
+    lid[hh] = (uint8_t)pi;
+    order();
+    const uint32_t w1 = lid[hh];
+    const bool loser = valid & (w1 != pi);
+    const uint64_t lmask = ballot(loser);
+    uint32_t ncut = 64, w2 = 0xffu;
+    uint64_t second = 0;                                          // lanes comparing to their group's first
+    if (lmask) {
+      // Round two reuses lid: only losers write, so a group without a
+      // loser still reads its winner back (w2 == w1).
+      lid[loser ? hh : kSink] = (uint8_t)pi;
       order();
-      const uint32_t w1 = lid[hh];
-      const bool loser = valid & (w1 != pi);
-      const uint64_t lmask = ballot(loser);
-      uint32_t ncut = 64, w2 = 0xffu;
-      uint64_t second = 0;                                        // lanes comparing to their group's first
-      if (lmask) {
-        // Round two reuses lid: only losers write, so a group without a
-        // loser still reads its winner back (w2 == w1).
-        lid[loser ? hh : kSink] = (uint8_t)pi;
-        order();
-        const uint32_t r2 = lid[hh];
-        w2 = r2 == w1 ? 0xffu : r2;                              // winners: 2nd member or none
-        const uint32_t wmax = w1 > r2 ? w1 : r2;
-        if (ballot(loser & (wmax > pi))) {                        // a group out of order
-          const uint32_t first = (uint32_t)__builtin_clzll(lmask); // earliest loser
-          ncut = first > 1 ? first : 1;
-        } else {
-          const uint64_t third = ballot(loser & (w2 != pi));
-          ncut = third ? (uint32_t)__builtin_clzll(third) : 64u;
-          second = lmask;
-          // A group's second probe compares against the first probe's
-          // bytes, which that lane already holds.
-          const uint32_t xfirst = __shfl(xv, 63 - (w1 & 63));
-          yv = loser ? xfirst : yv;
+      const uint32_t r2 = lid[hh];
+      w2 = r2 == w1 ? 0xffu : r2;                                // winners: 2nd member or none
+      const uint32_t wmax = w1 > r2 ? w1 : r2;
+      if (ballot(loser & (wmax > pi))) {                          // a group out of order
+        const uint32_t first = (uint32_t)__builtin_clzll(lmask);  // earliest loser
+        ncut = first > 1 ? first : 1;
+      } else {
+        const uint64_t third = ballot(loser & (w2 != pi));
+        ncut = third ? (uint32_t)__builtin_clzll(third) : 64u;
+        second = lmask;
+        // A group's second probe compares against the first probe's
+        // bytes, which that lane already holds.
+        const uint32_t xfirst = __shfl(xv, 63 - (w1 & 63));
+        yv = loser ? xfirst : yv;
+      }
+    }
+    const uint64_t mm = ballot((pi < ncut) & (xv == yv)) & vmask;     // snappy.c:152
+    const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
+    // snappy.c:148; a group's first probe defers to its second if both commit.
+    const bool shadowed = (second != 0) & !loser & (w2 < ncommit);
+    tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
+    order();
+
+    bool done;
+    if (mm) {
+      const uint32_t src = 63 - (ncommit - 1);
+      uint32_t at = lane_val(p, src);
+      uint32_t ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
+                                           : lane_val(ct, src);
+      // ---- copies, with lcdb's immediate re-match (snappy.c:158-187).
+      bool again;
+      do {
+        const uint32_t base = at;
+        uint32_t r = ref + 4;
+        at += 4;
+#pragma clang loop unroll(disable)
+        for (;;) {                                                // snappy.c:163-164
+          const uint32_t q = at + lane;
+          // Clamped unconditional reads (q < n implies r + lane < n).
+          const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
+          const bool same = (q < n) & (x[ra] == x[qa]);
+          const uint64_t diff = ballot(!same);
+          if (diff) {
+            at += (uint32_t)__builtin_ctzll(diff);
+            break;
+          }
+          at += kWave;
+          r += kWave;
         }
-      }
-      const uint64_t mm = ballot((pi < ncut) & (xv == yv)) & vmask;   // snappy.c:152
-      const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
-      // snappy.c:148; a group's first probe defers to its second if both commit.
-      const bool shadowed = (second != 0) & !loser & (w2 < ncommit);
-      tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
-      order();
-      if (mm) {
-        const uint32_t src = 63 - (ncommit - 1);
-        at = lane_val(p, src);
-        ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
-                                    : lane_val(ct, src);
-        break;
-      }
-      if ((uint32_t)__builtin_popcountll(vmask) < ncut) goto tail; // next probe past limit
+
+        // snappy.c:156 + 166: the literal before the copy, then the copy.
+        const uint32_t clen = at - base, dist = base - ref;
+        if (clen < 68) {
+          op += emit_seq(o, op, x, n, lit, base - lit, dist, clen);
+        } else {
+          op += emit_seq(o, op, x, n, lit, base - lit, 0, 0);
+          op += emit_copy(o, op, dist, clen);
+        }
+        lit = at;
+        done = at >= last;                                        // snappy.c:169
+        again = false;
+        if (!done) {
+          // snappy.c:172-180, as identical work on every lane (VALU + LDS
+          // broadcast).  lcdb's 64-bit compare (snappy.c:182): bytes
+          // at..at+6 against a zero-extended 4-byte load.
+          const uint32_t va = vec(at);
+          const uint64_t w = lds_ld64(x, va - 1);
+          const uint32_t h1 = hash32((uint32_t)w, shift), h2 = hash32((uint32_t)(w >> 8), shift);
+          tab[h1] = (uint16_t)(va - 1);
+          order();
+          const uint32_t c = tab[h2];
+          order();
+          tab[h2] = (uint16_t)va;
+          order();
+          again = ballot((w >> 8) == (uint64_t)lds_ld32(x, c)) != 0;
+          ref = uni(c);
+        }
+      } while (again);
+      start = at + 1;                                             // snappy.c:184-185
+      k = 0;
+    } else {
+      // No match in this batch: the search ends if a probe before the cut
+      // was past the limit, else continues after the cut.
+      done = (uint32_t)__builtin_popcountll(vmask) < ncut;
       k += ncut;
     }
-
-    // ---- copies, with lcdb's immediate re-match (snappy.c:158-187).
-    for (;;) {
-      const uint32_t base = at;
-      uint32_t r = ref + 4;
-      at += 4;
-#pragma clang loop unroll(disable)
-      for (;;) {                                                  // snappy.c:163-164
-        const uint32_t q = at + lane;
-        // Clamped unconditional reads (q < n implies r + lane < n).
-        const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
-        const bool same = (q < n) & (x[ra] == x[qa]);
-        const uint64_t diff = ballot(!same);
-        if (diff) {
-          at += (uint32_t)__builtin_ctzll(diff);
-          break;
-        }
-        at += kWave;
-        r += kWave;
-      }
-
-      // snappy.c:156 + 166: the literal before the copy, then the copy.
-      const uint32_t clen = at - base, dist = base - ref;
-      if (clen < 68) {
-        op += emit_seq(o, op, x, n, lit, base - lit, dist, clen);
-      } else {
-        op += emit_seq(o, op, x, n, lit, base - lit, 0, 0);
-        op += emit_copy(o, op, dist, clen);
-      }
-      lit = at;
-      if (at >= last) goto tail;                                  // snappy.c:169
-
-      // snappy.c:172-180, as identical work on every lane (VALU + LDS
-      // broadcast).  lcdb's 64-bit compare (snappy.c:182): bytes at..at+6
-      // against a zero-extended 4-byte load.
-      const uint32_t va = vec(at);
-      const uint64_t w = lds_ld64(x, va - 1);
-      const uint32_t h1 = hash32((uint32_t)w, shift), h2 = hash32((uint32_t)(w >> 8), shift);
-      tab[h1] = (uint16_t)(va - 1);
-      order();
-      const uint32_t c = tab[h2];
-      order();
-      tab[h2] = (uint16_t)va;
-      order();
-      if (ballot((w >> 8) != (uint64_t)lds_ld32(x, c))) {
-        ++at;
-        break;
-      }
-      ref = uni(c);
-    }
+    if (done) break;
   }
 
 tail:
