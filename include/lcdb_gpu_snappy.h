@@ -83,7 +83,10 @@ int lgs_encode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
 /* Device-resident decode.  Block i is d_in[d_in_off[i] .. + d_in_len[i]);
    it decodes into d_out + d_out_off[i] (capacity d_out_cap[i]);
    d_out_len[i] = decoded length (0 unless ok), d_status[i] = LGS_ST_*.
-   max_out_cap >= every d_out_cap[i].  Asynchronous on `stream`. */
+   max_out_cap >= every d_out_cap[i].  Asynchronous on `stream`.
+   Read slack: the kernel may READ (never write) up to 16 bytes past the end
+   of a block's input and past its output cursor, so both allocations must
+   extend at least 16 bytes beyond the last block. */
 int lgs_decode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
                          const uint32_t *d_in_len, uint8_t *d_out,
                          const uint64_t *d_out_off, const uint32_t *d_out_cap,

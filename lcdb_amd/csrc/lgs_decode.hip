@@ -272,15 +272,26 @@ __device__ __forceinline__ void flush_out(gptr<uint8_t> dst, const uint8_t* o, u
 // One LANE decodes one whole block, straight from HBM to HBM: the tag walk
 // is per-lane VALU code, so one instruction advances up to 64 blocks (the
 // wave-per-block kernel above is bound by the CU's single scalar unit:
-// ~60 SALU instructions per tag).  Byte moves are 16-byte unaligned
-// loads/stores.  Inside a block, writes may run up to 15 bytes past the
-// current op ("wild" chunks) because later ops overwrite them; they never
-// pass the block's end (the last chunk is written byte-exact).  A copy reads
-// bytes this lane stored earlier (same-work-item program order).
-// Overlapping copies (dist < len) use a byte broadcast for dist == 1 (all of
-// fillseq's) and a byte loop otherwise.
+// ~60 SALU instructions per tag).
 //
-// Inputs must be readable up to 16 bytes past each compressed block.
+// With 65 536 blocks a CU holds only ~4 such waves, so each block's serial
+// chain of ~180 tags is the critical path and what it costs per tag is
+// memory round trips.  Each tag therefore issues every load it needs at once
+// -- the 16-byte view of the NEXT tag and up to four 16-byte chunks of the
+// source (literal bytes from the input, or copy bytes from this block's
+// earlier output) -- and waits once.  vmcnt also counts stores and retires
+// in issue order, so a load issued after a store waits for it: a loop of
+// load/store pairs would pay one round trip per 16 bytes.
+//
+// Writes may run up to 15 bytes past the current op ("wild" chunks) because
+// later ops overwrite them; they never pass the block's end (the last chunk
+// is written byte-exact).  A copy reads bytes this lane stored earlier
+// (same-work-item program order).  Overlapping copies (dist < len) keep a
+// sequential path: dist == 1 broadcasts a byte (all of fillseq's), dist < 16
+// builds the period in registers, dist >= 16 copies chunk after chunk.
+//
+// Reads may touch 16 bytes past a block's input and past its output cursor
+// (see lgs_decode_batch_dev).
 // ---------------------------------------------------------------------------
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
@@ -290,7 +301,13 @@ __device__ __forceinline__ u32x4 ld16(gptr<const uint8_t> p) {
 __device__ __forceinline__ void st16(gptr<uint8_t> p, u32x4 v) { *(gptr<u32x4_u>)p = v; }
 
 __device__ __forceinline__ uint32_t pick(u32x4 v, uint32_t d) {   // v[d], d < 4
-  return d < 2 ? (d == 0 ? v.x : v.y) : (d == 2 ? v.z : v.w);
+  const uint32_t lo = d == 0 ? v.x : v.y;
+  const uint32_t hi = d == 2 ? v.z : v.w;
+  return d < 2 ? lo : hi;
+}
+
+__device__ __forceinline__ uint32_t byte_of(u32x4 v, uint32_t j) {   // byte j < 16
+  return (pick(v, j >> 2) >> (8 * (j & 3u))) & 0xffu;
 }
 
 // 8 bytes starting at p (>= 5 meaningful), via two aligned dword loads.
@@ -303,8 +320,20 @@ __device__ __forceinline__ uint64_t view8(gptr<const uint8_t> p) {
 
 // Store the first `len` bytes of the 16-byte value v at p, byte-exact.
 __device__ __forceinline__ void st_exact(gptr<uint8_t> p, u32x4 v, uint32_t len) {
-#pragma clang loop unroll(disable)
-  for (uint32_t b = 0; b < len; ++b) p[b] = (uint8_t)(pick(v, b >> 2) >> (8 * (b & 3u)));
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+  for (uint32_t b = 0; b < len; ++b) p[b] = (uint8_t)byte_of(v, b);
+}
+
+// Chunk k (16 bytes at d + 16k) of an op whose output ends `room` bytes
+// after d's block end would allow: wild when it fits, byte-exact otherwise.
+__device__ __forceinline__ void put16(gptr<uint8_t> d, u32x4 v, uint32_t k, uint32_t len,
+                                      uint32_t room) {
+  if (16 * k + 16 <= room) {
+    st16(d + 16 * k, v);
+  } else {
+    const uint32_t r = len - 16 * k;
+    st_exact(d + 16 * k, v, r < 16 ? r : 16);
+  }
 }
 
 template <uint32_t LANES>
@@ -341,13 +370,19 @@ __global__ __launch_bounds__(64) void decode_lane_kernel(
     if (want > cap) { st = 2; break; }
 
     uint32_t pos = hlen, made = 0;
-    uint64_t t = pos < slen ? view8(src + pos) : 0;
-    st = 1;
+    u32x4 tv = ld16(src + pos);                                 // bytes pos .. pos+15
+    // Settle that load here: left pending into the loop, it makes the
+    // compiler wait vmcnt(0) at the loop head on every tag -- i.e. for the
+    // previous tag's stores too.
+    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+    // A bad tag ends the walk by setting pos past slen (a sentinel rather
+    // than a status variable: one less loop-carried value, whose copy at
+    // the loop latch cost a vmcnt(0) -- i.e. waited for the tag's stores).
     while (pos < slen) {                                        // snappy.c:208
-      const uint32_t tag = (uint32_t)t & 0xffu;
+      const uint32_t tag = tv.x & 0xffu;
       const uint32_t kind = tag & 3u;
       const uint32_t left = slen - pos;
-      const uint32_t b1 = (uint32_t)(t >> 8);                  // bytes 1..4
+      const uint32_t b1 = (tv.x >> 8) | (tv.y << 24);           // bytes 1..4
       uint32_t len, hl, dist = 0;
       bool bad;
       if (kind == 0) {                                          // literal, snappy.c:210-273
@@ -379,42 +414,100 @@ __global__ __launch_bounds__(64) void decode_lane_kernel(
         bad = left < hl || dist == 0 || dist >= 0x80000000u || made < dist ||
               len > want - made;
       }
-      if (bad) { st = 0; break; }
+      if (bad) {
+        pos = 0xffffffffu;
+        break;
+      }
 
       const uint32_t next = pos + hl + (kind == 0 ? len : 0);
-      const uint64_t tn = next < slen ? view8(src + next) : 0;  // prefetch next tag
-
       const gptr<uint8_t> d = dst + made;
-      if (kind != 0 && dist < len) {
-        // Overlapping copy: the reference's forward byte loop repeats the
-        // dist-byte pattern (snappy.c:329-330).
-        if (dist == 1) {
-          const uint32_t b = d[-1];
-          const uint32_t w4 = b * 0x01010101u;
-          const u32x4 v = {w4, w4, w4, w4};
-#pragma clang loop unroll(disable)
-          for (uint32_t k = 0; k < len; k += 16) {
-            if (made + k + 16 <= want) st16(d + k, v);
-            else st_exact(d + k, v, len - k < 16 ? len - k : 16);
-          }
-        } else {
-#pragma clang loop unroll(disable)
-          for (uint32_t k = 0; k < len; ++k) d[k] = d[(int32_t)k - (int32_t)dist];
-        }
-      } else {
-        const gptr<const uint8_t> sp = kind == 0 ? src + pos + hl : (gptr<const uint8_t>)(d - dist);
-#pragma clang loop unroll(disable)
-        for (uint32_t k = 0; k < len; k += 16) {
-          const u32x4 v = ld16(sp + k);
-          if (made + k + 16 <= want) st16(d + k, v);
-          else st_exact(d + k, v, len - k < 16 ? len - k : 16);
-        }
+      const uint32_t room = want - made;                        // bytes writable from d
+      const bool overlap = kind != 0 && dist < len;
+      // Overlapping copies whose period divides 16 (dist 1, 2, 4, 8; every
+      // one in fillseq is dist 1) are a 16-byte register pattern and take
+      // the fast path with the rest; with 64 lanes some lane has one in most
+      // trips, so a slow path for them would be paid on most trips.
+      const bool pat = overlap && dist <= 8 && (dist & (dist - 1)) == 0;
+      const bool slow = overlap && !pat;
+      const gptr<const uint8_t> sp = kind == 0 ? src + pos + hl : (gptr<const uint8_t>)(d - dist);
+
+      // One round trip: the source chunks and the next tag's view together.
+      // (Zero-initialised, not copies of c0: a copy would make the compiler
+      // wait for c0 before issuing the rest.)
+      const u32x4 c0 = ld16(sp);
+      u32x4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;
+      if (!overlap) {
+        if (len > 16) c1 = ld16(sp + 16);
+        if (len > 32) c2 = ld16(sp + 32);
+        if (len > 48) c3 = ld16(sp + 48);
       }
+      const u32x4 tn = ld16(src + next);
+      // The tag's one wait.  Explicit, so that the compiler knows every chunk
+      // and the next view have arrived: its own waits in front of the
+      // (exec-masked, so not exactly countable) stores below would be
+      // vmcnt(1)s that wait for the previous store at each step.
+      __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
+
+      if (!slow) {
+        // Period-dist pattern from the dist bytes before d (c0's first bytes).
+        const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
+        const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
+        const uint32_t px = dist == 1 ? w1 : (dist == 2 ? w2 : c0.x);
+        const uint32_t py = dist == 8 ? c0.y : px;
+        const u32x4 pv = {px, py, px, py};
+        const u32x4 v0 = pat ? pv : c0, v1 = pat ? pv : c1, v2 = pat ? pv : c2,
+                    v3 = pat ? pv : c3;
+        put16(d, v0, 0, len, room);
+        if (len > 16) put16(d, v1, 1, len, room);
+        if (len > 32) put16(d, v2, 2, len, room);
+        if (len > 48) put16(d, v3, 3, len, room);
+        if (len > 64) {
+          // Literals longer than 64 bytes (copies never are): 64 bytes a trip.
+#pragma clang loop unroll(disable)
+          for (uint32_t k = 4; 16 * k < len; k += 4) {
+            const u32x4 e0 = ld16(sp + 16 * k);
+            u32x4 e1 = {0, 0, 0, 0}, e2 = e1, e3 = e1;
+            if (len > 16 * k + 16) e1 = ld16(sp + 16 * k + 16);
+            if (len > 16 * k + 32) e2 = ld16(sp + 16 * k + 32);
+            if (len > 16 * k + 48) e3 = ld16(sp + 16 * k + 48);
+            __builtin_amdgcn_s_waitcnt(0x0f70);
+            put16(d, e0, k, len, room);
+            if (len > 16 * k + 16) put16(d, e1, k + 1, len, room);
+            if (len > 16 * k + 32) put16(d, e2, k + 2, len, room);
+            if (len > 16 * k + 48) put16(d, e3, k + 3, len, room);
+          }
+        }
+      } else if (dist >= 16) {
+        // Overlapping, period >= 16: each chunk's source was written by an
+        // earlier chunk of this op (snappy.c:329-330 byte order).
+        put16(d, c0, 0, len, room);
+#pragma clang loop unroll(disable)
+        for (uint32_t k = 1; 16 * k < len; ++k) put16(d, ld16(sp + 16 * k), k, len, room);
+      } else {
+        // Overlapping, other periods < 16: p = the first 16 bytes of the
+        // pattern; bytes x and x - q agree for q = dist * ceil(16 / dist)
+        // >= 16, so later chunks copy from q back.
+        uint32_t w[4] = {0, 0, 0, 0};
+        uint32_t r = 0;
+#pragma clang loop unroll(disable)
+        for (uint32_t j = 0; j < 16; ++j) {
+          w[j >> 2] |= byte_of(c0, r) << (8 * (j & 3u));
+          r = r + 1 == dist ? 0 : r + 1;
+        }
+        put16(d, u32x4{w[0], w[1], w[2], w[3]}, 0, len, room);
+        const uint32_t q = dist * ((16 + dist - 1) / dist);
+#pragma clang loop unroll(disable)
+        for (uint32_t k = 1; 16 * k < len; ++k)
+          put16(d, ld16((gptr<const uint8_t>)(d + 16 * k - q)), k, len, room);
+      }
+      // Nothing left in flight that a register is waiting for (keeps the
+      // compiler from waiting at the loop head, behind this tag's stores).
+      if (slow || len > 64) __builtin_amdgcn_s_waitcnt(0x0f70);
       made += len;
       pos = next;
-      t = tn;
+      tv = tn;
     }
-    if (st == 1 && made != want) st = 0;                       // snappy.c:337
+    st = (pos == slen && made == want) ? 1u : 0u;              // snappy.c:208, :337
   } while (0);
 
   status[i] = (uint8_t)st;

@@ -115,51 +115,54 @@ __device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uin
   return total;
 }
 
-// snappy.c:53-102, the common case in one pass: the pending literal
-// x[lit .. lit+L) (L == 0: none) followed by a copy of length C < 68 at
-// distance D (C == 0: none).  Lane b writes byte b of the sequence.  The
-// header and tag arithmetic runs on the VALU (vec()), selects replace
-// branches, and lanes past the end store at an out-of-range offset that the
-// buffer range check drops, so the pass has no exec-mask regions (their
-// save/restore is scalar work, and the scalar unit is what this kernel
-// saturates).  Returns bytes written.
-__device__ __forceinline__ uint32_t emit_seq(const OutSlot& o, uint32_t op, const uint8_t* x,
-                                             uint32_t n, uint32_t lit, uint32_t L, uint32_t D,
-                                             uint32_t C) {
-  // Every ?: below picks between values already computed: clang lowers a
-  // conditional whose arms still hold work to branches (exec-mask regions).
-  const uint32_t lane = lane_id();
-  const uint32_t vL = vec(L), vD = vec(D), vC = vec(C), vlit = vec(lit);
-  const uint32_t m = vL - 1;                                          // snappy.c:55-66
-  const uint32_t hl_big = m < 256 ? 2u : 3u;
-  const uint32_t hl_any = m < 60 ? 1u : hl_big;
-  const uint32_t hl = vL == 0 ? 0u : hl_any;
-  const uint32_t h0_big = m < 256 ? 0xf0u : 0xf4u;
-  const uint32_t m4 = m << 2;
-  const uint32_t h0 = m < 60 ? m4 : h0_big;
-  const uint32_t hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);
-  const uint32_t has60 = vC > 64 ? 3u : 0u;                           // snappy.c:84-89
-  const uint32_t rest = vC - 20 * has60;
-  // rest < 12 && D < 2048 (snappy.c:91), as sign bits: no lane-mask logic.
-  const bool c1 = (int32_t)((rest - 12) & (vD - 2048)) < 0;
-  const uint32_t f1 = ((vD >> 8) << 5) | ((rest - 4) << 2) | 1u;      // snappy.c:98
-  const uint32_t f2 = ((rest - 1) << 2) | 2u;                         // snappy.c:92
-  const uint32_t first = c1 ? f1 : f2;
-  const uint32_t ntag = c1 ? 2u : 3u;
-  const uint32_t ctag = has60 + ntag;
-  const uint32_t ctot = vC == 0 ? 0u : ctag;
-  const uint32_t lend = hl + vL;                                      // first copy byte
-  const uint32_t vtotal = lend + ctot;
-  const uint32_t dlo = vD, dhi = vD >> 8;
-  const uint32_t total = uni(vtotal);
-#pragma clang loop unroll(disable) vectorize(disable)
-  for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
-    const uint32_t b = vec(j0) + lane;
+// snappy.c:53-102, the common case: the pending literal x[lit .. lit+L)
+// (L == 0: none) followed by a copy of length C < 68 at distance D (C == 0:
+// none), written 64 bytes a pass: lane b writes byte b of the sequence.
+// The header and tag arithmetic runs on the VALU (vec()), and every ?:
+// picks between values already computed (clang lowers a conditional whose
+// arms still hold work to exec-mask branches, whose save/restore is scalar
+// work -- and the scalar unit is what this kernel saturates).  Lanes past
+// the end store at an out-of-range offset that the buffer range check
+// drops.  pass(0) is straight-line code the caller can place next to other
+// LDS work; total > 64 needs further passes (rare).
+struct Seq {
+  uint32_t vL, vD, vlit, hl, hdr, has60, first, lend, vtotal, total;
+  __device__ __forceinline__ Seq(uint32_t lit, uint32_t L, uint32_t D, uint32_t C) {
+    vL = vec(L);
+    vD = vec(D);
+    vlit = vec(lit);
+    const uint32_t vC = vec(C);
+    const uint32_t m = vL - 1;                                        // snappy.c:55-66
+    const uint32_t hl_big = m < 256 ? 2u : 3u;
+    const uint32_t hl_any = m < 60 ? 1u : hl_big;
+    hl = vL == 0 ? 0u : hl_any;
+    const uint32_t h0_big = m < 256 ? 0xf0u : 0xf4u;
+    const uint32_t m4 = m << 2;
+    const uint32_t h0 = m < 60 ? m4 : h0_big;
+    hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);
+    has60 = vC > 64 ? 3u : 0u;                                        // snappy.c:84-89
+    const uint32_t rest = vC - 20 * has60;
+    // rest < 12 && D < 2048 (snappy.c:91), as sign bits: no lane-mask logic.
+    const bool c1 = (int32_t)((rest - 12) & (vD - 2048)) < 0;
+    const uint32_t f1 = ((vD >> 8) << 5) | ((rest - 4) << 2) | 1u;    // snappy.c:98
+    const uint32_t f2 = ((rest - 1) << 2) | 2u;                       // snappy.c:92
+    first = c1 ? f1 : f2;
+    const uint32_t ntag = c1 ? 2u : 3u;
+    const uint32_t ctag = has60 + ntag;
+    const uint32_t ctot = vC == 0 ? 0u : ctag;
+    lend = hl + vL;                                                   // first copy byte
+    vtotal = lend + ctot;
+    total = uni(vtotal);
+  }
+  __device__ __forceinline__ void pass(const OutSlot& o, uint32_t op, const uint8_t* x,
+                                       uint32_t n, uint32_t j0) const {
+    const uint32_t b = vec(j0) + lane_id();
     const uint32_t ia = vlit + b - hl;                                // underflows for b < hl
     const uint32_t iac = ia < n ? ia : n;
     const uint32_t lb = x[iac];
     const uint32_t cb = b - lend;                                     // byte of the copy tags
     const uint32_t r = cb - has60;
+    const uint32_t dlo = vD, dhi = vD >> 8;
     const uint32_t t60 = cb == 1 ? dlo : dhi;
     const uint32_t p60 = cb == 0 ? 0xeeu : t60;                       // the 60-byte piece
     const uint32_t tr = r == 1 ? dlo : dhi;
@@ -171,8 +174,12 @@ __device__ __forceinline__ uint32_t emit_seq(const OutSlot& o, uint32_t op, cons
     const uint32_t voff = b < vtotal ? b : 0x40000000u;               // dropped by the range check
     o.put(op, voff, v);
   }
-  return total;
-}
+  __device__ __forceinline__ void rest(const OutSlot& o, uint32_t op, const uint8_t* x,
+                                       uint32_t n) const {
+#pragma clang loop unroll(disable) vectorize(disable)
+    for (uint32_t j0 = kWave; j0 < total; j0 += kWave) pass(o, op, x, n, j0);
+  }
+};
 
 // Index of the scratch slot every table / lane-id array carries past its
 // 2048 real entries: lanes that must not touch a real entry write there
@@ -237,6 +244,11 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
       const uint32_t kc = in_tab ? kk : kProbeTab - 1;
       o0 = kProbe.off[kc];
       o1 = kProbe.off[kc + 1];
+      // Wait for these two loads here, on the rare path.  Left to the
+      // compiler, the wait lands where the paths merge as vmcnt(0) -- and
+      // vmcnt also counts the output stores, so every batch would stall
+      // until the previous copy's bytes had reached memory.
+      __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
     }
     const bool valid = in_tab && start + o1 <= last;              // snappy.c:143
     const uint64_t vmask = ballot(valid);
@@ -310,33 +322,35 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
           r += kWave;
         }
 
-        // snappy.c:156 + 166: the literal before the copy, then the copy.
+        // snappy.c:156 + 166: the literal before the copy, then the copy
+        // (copies of 68+ bytes, rare, get their tags from emit_copy).
         const uint32_t clen = at - base, dist = base - ref;
-        if (clen < 68) {
-          op += emit_seq(o, op, x, n, lit, base - lit, dist, clen);
-        } else {
-          op += emit_seq(o, op, x, n, lit, base - lit, 0, 0);
-          op += emit_copy(o, op, dist, clen);
-        }
-        lit = at;
+        const bool longc = clen >= 68;
+        const Seq sq(lit, base - lit, longc ? 0u : dist, longc ? 0u : clen);
+        sq.pass(o, op, x, n, 0);
+
         done = at >= last;                                        // snappy.c:169
-        again = false;
-        if (!done) {
-          // snappy.c:172-180, as identical work on every lane (VALU + LDS
-          // broadcast).  lcdb's 64-bit compare (snappy.c:182): bytes
-          // at..at+6 against a zero-extended 4-byte load.
-          const uint32_t va = vec(at);
-          const uint64_t w = lds_ld64(x, va - 1);
-          const uint32_t h1 = hash32((uint32_t)w, shift), h2 = hash32((uint32_t)(w >> 8), shift);
-          tab[h1] = (uint16_t)(va - 1);
-          order();
-          const uint32_t c = tab[h2];
-          order();
-          tab[h2] = (uint16_t)va;
-          order();
-          again = ballot((w >> 8) == (uint64_t)lds_ld32(x, c)) != 0;
-          ref = uni(c);
-        }
+        // snappy.c:172-180, as identical work on every lane (VALU + LDS
+        // broadcast), run even when `done` (the table is dead then, and the
+        // reads stay inside the LDS pad) so that it has no branch around it
+        // and the scheduler can overlap it with the emission pass above.
+        // Every lane does the same work, so single-thread program order is
+        // the real order: no order() barriers.  lcdb's 64-bit compare
+        // (snappy.c:182): bytes at..at+6 against a zero-extended 4-byte load.
+        const uint32_t va = vec(at);
+        const uint64_t w = lds_ld64(x, va - 1);
+        const uint32_t h1 = hash32((uint32_t)w, shift), h2 = hash32((uint32_t)(w >> 8), shift);
+        tab[h1] = (uint16_t)(va - 1);
+        const uint32_t c = tab[h2];
+        tab[h2] = (uint16_t)va;
+        const bool hit = ballot((w >> 8) == (uint64_t)lds_ld32(x, c)) != 0;
+        again = !done && hit;
+        ref = uni(c);
+
+        sq.rest(o, op, x, n);
+        op += sq.total;
+        if (longc) op += emit_copy(o, op, dist, clen);
+        lit = at;
       } while (again);
       start = at + 1;                                             // snappy.c:184-185
       k = 0;
@@ -349,7 +363,6 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
     if (done) break;
   }
 
-tail:
   if (lit < n) op += emit_literal(o, op, x, lit, n - lit);         // snappy.c:190-192
   return op;
 }
@@ -376,6 +389,10 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   const uint32_t lane = lane_id();
   // Probe offsets of the first 64 probes of a search, kept in registers.
   const uint32_t off0 = kProbe.off[63 - lane], off1 = kProbe.off[64 - lane];
+  // Settle these loads now: otherwise the compiler cannot prove them done
+  // inside the batch loop and waits vmcnt(0) there -- on every batch, behind
+  // every pending output store.
+  __builtin_amdgcn_s_waitcnt(0x0f70);                             // vmcnt(0)
 
   const uint32_t len = uni(in_len[i]);
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
