@@ -319,9 +319,18 @@ __device__ __forceinline__ uint64_t view8(gptr<const uint8_t> p) {
 }
 
 // Store the first `len` bytes of the 16-byte value v at p, byte-exact.
+// The byte stores are inline asm: written as C++ they made the compiler's
+// wait-count analysis put a vmcnt(0) at the head of the decode loop (paid on
+// every tag, i.e. waiting for that tag's stores), although nothing a later
+// instruction reads is in flight.  The trailing s_nop covers the VMEM-store
+// data hazard, which the hazard recognizer cannot see through inline asm.
 __device__ __forceinline__ void st_exact(gptr<uint8_t> p, u32x4 v, uint32_t len) {
 #pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
-  for (uint32_t b = 0; b < len; ++b) p[b] = (uint8_t)byte_of(v, b);
+  for (uint32_t b = 0; b < len; ++b) {
+    const uint32_t byte = byte_of(v, b);
+    asm volatile("global_store_byte %0, %1, off\n\ts_nop 1" ::"v"(p + b), "v"(byte)
+                 : "memory");
+  }
 }
 
 // Chunk k (16 bytes at d + 16k) of an op whose output ends `room` bytes
@@ -334,6 +343,148 @@ __device__ __forceinline__ void put16(gptr<uint8_t> d, u32x4 v, uint32_t k, uint
     const uint32_t r = len - 16 * k;
     st_exact(d + 16 * k, v, r < 16 ? r : 16);
   }
+}
+
+// One parsed tag (snappy.c:210-324) of a lane's stream.
+struct Tag {
+  uint32_t kind, len, hl, dist, next;
+  bool bad;
+};
+
+__device__ __forceinline__ Tag parse_tag(u32x4 tv, uint32_t pos, uint32_t slen, uint32_t want,
+                                         uint32_t made) {
+  Tag t;
+  const uint32_t tag = tv.x & 0xffu;
+  t.kind = tag & 3u;
+  const uint32_t left = slen - pos;
+  const uint32_t b1 = (tv.x >> 8) | (tv.y << 24);              // bytes 1..4
+  t.dist = 0;
+  if (t.kind == 0) {                                            // literal, snappy.c:210-273
+    uint32_t m = tag >> 2;
+    t.hl = 1;
+    t.bad = false;
+    if (m >= 60) {
+      const uint32_t extra = m - 59;
+      t.bad = left - 1 < extra;
+      m = extra == 4 ? b1 : (b1 & ((1u << (8 * extra)) - 1u));
+      t.hl += extra;
+    }
+    t.len = m + 1;
+    t.bad = t.bad || m >= 0x7fffffffu || t.len > want - made || t.len > left - t.hl;
+  } else {                                                      // snappy.c:276-324
+    if (t.kind == 1) {
+      t.len = 4 + ((tag >> 2) & 7u);
+      t.dist = ((tag & 0xe0u) << 3) | (b1 & 0xffu);
+      t.hl = 2;
+    } else if (t.kind == 2) {
+      t.len = 1 + (tag >> 2);
+      t.dist = b1 & 0xffffu;
+      t.hl = 3;
+    } else {
+      t.len = 1 + (tag >> 2);
+      t.dist = b1;
+      t.hl = 5;
+    }
+    t.bad = left < t.hl || t.dist == 0 || t.dist >= 0x80000000u || made < t.dist ||
+            t.len > want - made;
+  }
+  t.next = pos + t.hl + (t.kind == 0 ? t.len : 0);
+  return t;
+}
+
+// Overlapping copies whose period does not divide 16 (dist 3, 5-7, 9-15)
+// or is >= 16: the only ops the fast path does not take.
+__device__ __forceinline__ bool tag_slow(const Tag& t) {
+  return t.kind != 0 && t.dist < t.len && !(t.dist <= 8 && (t.dist & (t.dist - 1)) == 0);
+}
+
+// Fast path for one tag: every load it needs (up to four 16-byte source
+// chunks and the next tag's view) in one round trip, one explicit wait,
+// then the stores.  Literals over 64 bytes continue 64 bytes a trip.
+// Returns the next tag's view.
+__device__ __forceinline__ u32x4 fast_op(const Tag& t, gptr<const uint8_t> src, uint32_t pos,
+                                         gptr<uint8_t> d, uint32_t room) {
+  const uint32_t len = t.len, dist = t.dist;
+  const bool overlap = t.kind != 0 && dist < len;               // dist 1, 2, 4 or 8 here
+  const gptr<const uint8_t> sp = t.kind == 0 ? src + pos + t.hl : (gptr<const uint8_t>)(d - dist);
+  // (Zero-initialised, not copies of c0: a copy would make the compiler wait
+  // for c0 before issuing the rest.)
+  const u32x4 c0 = ld16(sp);
+  u32x4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;
+  if (!overlap) {
+    if (len > 16) c1 = ld16(sp + 16);
+    if (len > 32) c2 = ld16(sp + 32);
+    if (len > 48) c3 = ld16(sp + 48);
+  }
+  const u32x4 tn = ld16(src + t.next);
+  // The tag's one wait.  Explicit, so that the compiler knows every chunk
+  // and the next view have arrived: its own waits in front of the
+  // (exec-masked, so not exactly countable) stores below would be vmcnt(1)s
+  // that wait for the previous store at each step.
+  __builtin_amdgcn_s_waitcnt(0x0f70);                           // vmcnt(0)
+
+  // Overlapping copies of period 1/2/4/8 (every one in fillseq is dist 1):
+  // the pattern of the dist bytes before d, as a 16-byte register.
+  const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
+  const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
+  const uint32_t px = dist == 1 ? w1 : (dist == 2 ? w2 : c0.x);
+  const uint32_t py = dist == 8 ? c0.y : px;
+  const u32x4 pv = {px, py, px, py};
+  const u32x4 v0 = overlap ? pv : c0, v1 = overlap ? pv : c1, v2 = overlap ? pv : c2,
+              v3 = overlap ? pv : c3;
+  put16(d, v0, 0, len, room);
+  if (len > 16) put16(d, v1, 1, len, room);
+  if (len > 32) put16(d, v2, 2, len, room);
+  if (len > 48) put16(d, v3, 3, len, room);
+  if (len > 64) {
+    // Literals longer than 64 bytes (copies never are).
+#pragma clang loop unroll(disable)
+    for (uint32_t k = 4; 16 * k < len; k += 4) {
+      const u32x4 e0 = ld16(sp + 16 * k);
+      u32x4 e1 = {0, 0, 0, 0}, e2 = e1, e3 = e1;
+      if (len > 16 * k + 16) e1 = ld16(sp + 16 * k + 16);
+      if (len > 16 * k + 32) e2 = ld16(sp + 16 * k + 32);
+      if (len > 16 * k + 48) e3 = ld16(sp + 16 * k + 48);
+      __builtin_amdgcn_s_waitcnt(0x0f70);
+      put16(d, e0, k, len, room);
+      if (len > 16 * k + 16) put16(d, e1, k + 1, len, room);
+      if (len > 16 * k + 32) put16(d, e2, k + 2, len, room);
+      if (len > 16 * k + 48) put16(d, e3, k + 3, len, room);
+    }
+  }
+  return tn;
+}
+
+// Slow path: overlapping copies of other periods, in the reference's byte
+// order (snappy.c:329-330).  Returns the next tag's view.
+__device__ __noinline__ u32x4 slow_op(const Tag& t, gptr<const uint8_t> src, gptr<uint8_t> d,
+                                      uint32_t room) {
+  const uint32_t len = t.len, dist = t.dist;
+  const gptr<const uint8_t> sp = (gptr<const uint8_t>)(d - dist);
+  if (dist >= 16) {
+    // Each chunk's source was written by an earlier chunk of this op.
+#pragma clang loop unroll(disable)
+    for (uint32_t k = 0; 16 * k < len; ++k) put16(d, ld16(sp + 16 * k), k, len, room);
+  } else {
+    // p = the first 16 bytes of the pattern; bytes x and x - q agree for
+    // q = dist * ceil(16 / dist) >= 16, so later chunks copy from q back.
+    const u32x4 c0 = ld16(sp);
+    uint32_t w[4] = {0, 0, 0, 0};
+    uint32_t r = 0;
+#pragma clang loop unroll(disable)
+    for (uint32_t j = 0; j < 16; ++j) {
+      w[j >> 2] |= byte_of(c0, r) << (8 * (j & 3u));
+      r = r + 1 == dist ? 0 : r + 1;
+    }
+    put16(d, u32x4{w[0], w[1], w[2], w[3]}, 0, len, room);
+    const uint32_t q = dist * ((16 + dist - 1) / dist);
+#pragma clang loop unroll(disable)
+    for (uint32_t k = 1; 16 * k < len; ++k)
+      put16(d, ld16((gptr<const uint8_t>)(d + 16 * k - q)), k, len, room);
+  }
+  const u32x4 tn = ld16(src + t.next);
+  __builtin_amdgcn_s_waitcnt(0x0f70);
+  return tn;
 }
 
 template <uint32_t LANES>
@@ -352,11 +503,10 @@ __global__ __launch_bounds__(64) void decode_lane_kernel(
   const gptr<uint8_t> dst = to_global(out) + out_off[i];
   const uint32_t cap = out_cap[i];
 
-  uint32_t st = 0, want = 0;
-  do {
-    // varint32 header, coding.h:169-204.
+  // varint32 header, coding.h:169-204.
+  uint32_t st = 1, want = 0, hlen = 0;
+  {
     const uint64_t h = view8(src);
-    uint32_t hlen = 0;
     for (uint32_t k = 0; k < 5 && k < slen; ++k) {
       const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
       if ((b & 0x80u) == 0) {
@@ -366,149 +516,56 @@ __global__ __launch_bounds__(64) void decode_lane_kernel(
       }
       want |= (b & 0x7fu) << (7 * k);
     }
-    if (hlen == 0 || want > 0x7fffffffu) { st = 0; break; }   // snappy.c:405-409
-    if (want > cap) { st = 2; break; }
+    if (hlen == 0 || want > 0x7fffffffu) st = 0;                // snappy.c:405-409
+    else if (want > cap) st = 2;
+    want = st == 1 ? want : 0;
+  }
+  // A lane that is not decoding (bad header, or done) has pos >= slen; a bad
+  // tag sets pos to a sentinel past slen (a sentinel rather than a status
+  // variable: one less loop-carried value).
+  uint32_t pos = st == 1 ? hlen : 0xffffffffu;
+  uint32_t made = 0;
+  u32x4 tv = ld16(src + (st == 1 ? pos : 0));
+  // Settle that load here: left pending into the loop, it makes the
+  // compiler wait vmcnt(0) at the loop head on every tag -- i.e. for the
+  // previous tag's stores too.
+  __builtin_amdgcn_s_waitcnt(0x0f70);
 
-    uint32_t pos = hlen, made = 0;
-    u32x4 tv = ld16(src + pos);                                 // bytes pos .. pos+15
-    // Settle that load here: left pending into the loop, it makes the
-    // compiler wait vmcnt(0) at the loop head on every tag -- i.e. for the
-    // previous tag's stores too.
-    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
-    // A bad tag ends the walk by setting pos past slen (a sentinel rather
-    // than a status variable: one less loop-carried value, whose copy at
-    // the loop latch cost a vmcnt(0) -- i.e. waited for the tag's stores).
-    while (pos < slen) {                                        // snappy.c:208
-      const uint32_t tag = tv.x & 0xffu;
-      const uint32_t kind = tag & 3u;
-      const uint32_t left = slen - pos;
-      const uint32_t b1 = (tv.x >> 8) | (tv.y << 24);           // bytes 1..4
-      uint32_t len, hl, dist = 0;
-      bool bad;
-      if (kind == 0) {                                          // literal, snappy.c:210-273
-        uint32_t m = tag >> 2;
-        hl = 1;
-        bad = false;
-        if (m >= 60) {
-          const uint32_t extra = m - 59;
-          bad = left - 1 < extra;
-          m = extra == 4 ? b1 : (b1 & ((1u << (8 * extra)) - 1u));
-          hl += extra;
-        }
-        len = m + 1;
-        bad = bad || m >= 0x7fffffffu || len > want - made || len > left - hl;
-      } else {                                                  // snappy.c:276-324
-        if (kind == 1) {
-          len = 4 + ((tag >> 2) & 7u);
-          dist = ((tag & 0xe0u) << 3) | (b1 & 0xffu);
-          hl = 2;
-        } else if (kind == 2) {
-          len = 1 + (tag >> 2);
-          dist = b1 & 0xffffu;
-          hl = 3;
-        } else {
-          len = 1 + (tag >> 2);
-          dist = b1;
-          hl = 5;
-        }
-        bad = left < hl || dist == 0 || dist >= 0x80000000u || made < dist ||
-              len > want - made;
-      }
-      if (bad) {
+  // Fast trips until some lane's next tag needs the slow path; then one
+  // trip in which every live lane does its op (slow or fast); repeat.  The
+  // fast loop holds no slow-path code, so the compiler's wait analysis sees
+  // nothing in flight at its head (a wait there would also wait for the
+  // previous tag's stores).
+  for (;;) {
+    Tag t;
+    bool live, slow_trip = false;
+    for (;;) {                                                  // snappy.c:208
+      live = pos < slen;
+      if (ballot(live) == 0) break;
+      t = parse_tag(tv, pos, slen, want, made);
+      if (live && t.bad) {
         pos = 0xffffffffu;
+        live = false;
+      }
+      if (ballot(live && tag_slow(t))) {
+        slow_trip = true;
         break;
       }
-
-      const uint32_t next = pos + hl + (kind == 0 ? len : 0);
-      const gptr<uint8_t> d = dst + made;
-      const uint32_t room = want - made;                        // bytes writable from d
-      const bool overlap = kind != 0 && dist < len;
-      // Overlapping copies whose period divides 16 (dist 1, 2, 4, 8; every
-      // one in fillseq is dist 1) are a 16-byte register pattern and take
-      // the fast path with the rest; with 64 lanes some lane has one in most
-      // trips, so a slow path for them would be paid on most trips.
-      const bool pat = overlap && dist <= 8 && (dist & (dist - 1)) == 0;
-      const bool slow = overlap && !pat;
-      const gptr<const uint8_t> sp = kind == 0 ? src + pos + hl : (gptr<const uint8_t>)(d - dist);
-
-      // One round trip: the source chunks and the next tag's view together.
-      // (Zero-initialised, not copies of c0: a copy would make the compiler
-      // wait for c0 before issuing the rest.)
-      const u32x4 c0 = ld16(sp);
-      u32x4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;
-      if (!overlap) {
-        if (len > 16) c1 = ld16(sp + 16);
-        if (len > 32) c2 = ld16(sp + 32);
-        if (len > 48) c3 = ld16(sp + 48);
+      if (live) {
+        tv = fast_op(t, src, pos, dst + made, want - made);
+        made += t.len;
+        pos = t.next;
       }
-      const u32x4 tn = ld16(src + next);
-      // The tag's one wait.  Explicit, so that the compiler knows every chunk
-      // and the next view have arrived: its own waits in front of the
-      // (exec-masked, so not exactly countable) stores below would be
-      // vmcnt(1)s that wait for the previous store at each step.
-      __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
-
-      if (!slow) {
-        // Period-dist pattern from the dist bytes before d (c0's first bytes).
-        const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
-        const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
-        const uint32_t px = dist == 1 ? w1 : (dist == 2 ? w2 : c0.x);
-        const uint32_t py = dist == 8 ? c0.y : px;
-        const u32x4 pv = {px, py, px, py};
-        const u32x4 v0 = pat ? pv : c0, v1 = pat ? pv : c1, v2 = pat ? pv : c2,
-                    v3 = pat ? pv : c3;
-        put16(d, v0, 0, len, room);
-        if (len > 16) put16(d, v1, 1, len, room);
-        if (len > 32) put16(d, v2, 2, len, room);
-        if (len > 48) put16(d, v3, 3, len, room);
-        if (len > 64) {
-          // Literals longer than 64 bytes (copies never are): 64 bytes a trip.
-#pragma clang loop unroll(disable)
-          for (uint32_t k = 4; 16 * k < len; k += 4) {
-            const u32x4 e0 = ld16(sp + 16 * k);
-            u32x4 e1 = {0, 0, 0, 0}, e2 = e1, e3 = e1;
-            if (len > 16 * k + 16) e1 = ld16(sp + 16 * k + 16);
-            if (len > 16 * k + 32) e2 = ld16(sp + 16 * k + 32);
-            if (len > 16 * k + 48) e3 = ld16(sp + 16 * k + 48);
-            __builtin_amdgcn_s_waitcnt(0x0f70);
-            put16(d, e0, k, len, room);
-            if (len > 16 * k + 16) put16(d, e1, k + 1, len, room);
-            if (len > 16 * k + 32) put16(d, e2, k + 2, len, room);
-            if (len > 16 * k + 48) put16(d, e3, k + 3, len, room);
-          }
-        }
-      } else if (dist >= 16) {
-        // Overlapping, period >= 16: each chunk's source was written by an
-        // earlier chunk of this op (snappy.c:329-330 byte order).
-        put16(d, c0, 0, len, room);
-#pragma clang loop unroll(disable)
-        for (uint32_t k = 1; 16 * k < len; ++k) put16(d, ld16(sp + 16 * k), k, len, room);
-      } else {
-        // Overlapping, other periods < 16: p = the first 16 bytes of the
-        // pattern; bytes x and x - q agree for q = dist * ceil(16 / dist)
-        // >= 16, so later chunks copy from q back.
-        uint32_t w[4] = {0, 0, 0, 0};
-        uint32_t r = 0;
-#pragma clang loop unroll(disable)
-        for (uint32_t j = 0; j < 16; ++j) {
-          w[j >> 2] |= byte_of(c0, r) << (8 * (j & 3u));
-          r = r + 1 == dist ? 0 : r + 1;
-        }
-        put16(d, u32x4{w[0], w[1], w[2], w[3]}, 0, len, room);
-        const uint32_t q = dist * ((16 + dist - 1) / dist);
-#pragma clang loop unroll(disable)
-        for (uint32_t k = 1; 16 * k < len; ++k)
-          put16(d, ld16((gptr<const uint8_t>)(d + 16 * k - q)), k, len, room);
-      }
-      // Nothing left in flight that a register is waiting for (keeps the
-      // compiler from waiting at the loop head, behind this tag's stores).
-      if (slow || len > 64) __builtin_amdgcn_s_waitcnt(0x0f70);
-      made += len;
-      pos = next;
-      tv = tn;
     }
-    st = (pos == slen && made == want) ? 1u : 0u;              // snappy.c:208, :337
-  } while (0);
+    if (!slow_trip) break;
+    if (live) {
+      tv = tag_slow(t) ? slow_op(t, src, dst + made, want - made)
+                       : fast_op(t, src, pos, dst + made, want - made);
+      made += t.len;
+      pos = t.next;
+    }
+  }
+  if (st == 1) st = (pos == slen && made == want) ? 1u : 0u;   // snappy.c:208, :337
 
   status[i] = (uint8_t)st;
   out_len[i] = st == 1 ? want : 0;
