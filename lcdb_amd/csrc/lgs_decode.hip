@@ -719,6 +719,303 @@ static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
 }
 
 // Class limits (bytes of decoded output held in LDS per wave).
+// ---------------------------------------------------------------------------
+// Ring decoder: lane-per-block with LDS staging (large batches).
+//
+// The lane kernel above moves every byte as a 16-byte access of its own
+// lane, so each memory instruction touches 64 cache lines: on C2 the
+// texture addresser is ~93 % busy and partially written lines are evicted
+// and rewritten (3.4x the output bytes reach HBM).  Here each lane keeps
+//   * an input window: a 128-byte ring of its compressed stream, refilled
+//     64 bytes at a time by 4 cooperating lanes (one coalesced line), and
+//   * an output ring of 256 bytes, flushed 128 bytes at a time by 8
+//     cooperating lanes (whole lines, written once),
+// both in LDS with a 64-byte mirror after the ring so that any read of up
+// to 64 bytes from a ring offset is linear.  Literals and copies with
+// dist <= kNear move LDS to LDS; farther copies read the already flushed
+// output from memory, issued when the tag is parsed and used a trip later.
+// A trip = one piece (<= 64 bytes) of one op per lane; every memory
+// operation issued in a trip is waited for once, at the top of the next.
+// ---------------------------------------------------------------------------
+namespace ring {
+constexpr uint32_t kInRing = 128, kInStride = 208;     // ring + 64 mirror + 16 sink
+constexpr uint32_t kOutRing = 256, kOutStride = 352;   // 16 pad + ring + 64 mirror + 16
+constexpr uint32_t kNear = 240;                         // ring minus one wild chunk
+constexpr uint32_t kFlush = 128;
+constexpr uint32_t kInSink = kInRing + 64;             // a lane's sink slot (its slack)
+}  // namespace ring
+
+typedef u32x4 u32x4_l1 __attribute__((aligned(1)));
+__device__ __forceinline__ u32x4 lrd16(const uint8_t* p) { return *(const u32x4_l1*)p; }
+__device__ __forceinline__ void lwr16(uint8_t* p, u32x4 v) { *(u32x4_l1*)p = v; }
+
+// 16 bytes at output offset p of a lane's ring (ob = ring start): the ring
+// copy, plus the mirror copy (r < 64) or the wrapped part (r > 240); lanes
+// with neither write the pad in front of the ring.
+__device__ __forceinline__ void out_put(uint8_t* ob, uint32_t p, u32x4 v) {
+  const uint32_t r = p & (ring::kOutRing - 1);
+  lwr16(ob + r, v);
+  const int32_t r2 = r < 64 ? (int32_t)r + 256 : (r > 240 ? (int32_t)r - 256 : -16);
+  lwr16(ob + r2, v);
+}
+
+struct RingJob {   // 32 bytes
+  uint32_t lane, off, cnt, plo, phi, pad0, pad1, pad2;
+};
+
+__global__ __launch_bounds__(64) void decode_ring_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n) {
+  using namespace ring;
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[64 * kInStride];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * kOutStride];
+  __shared__ __attribute__((aligned(16))) RingJob s_job[64];
+
+  // Every lane stays to the end: lanes without a block still work for the
+  // cooperative refills and flushes.
+  const uint32_t lane = threadIdx.x;
+  const uint32_t slot = blockIdx.x * 64 + lane;
+  const bool exists = slot < n;
+  const uint32_t i = exists ? (index ? index[slot] : slot) : 0;
+  const gptr<const uint8_t> src = to_global(in) + (exists ? in_off[i] : 0);
+  const uint32_t slen = exists ? in_len[i] : 0;
+  const gptr<uint8_t> dst = to_global(out) + (exists ? out_off[i] : 0);
+  const uint32_t cap = exists ? out_cap[i] : 0;
+  uint8_t* const ib = s_in + lane * kInStride;
+  uint8_t* const ob = s_out + lane * kOutStride + 16;
+
+  // varint32 header, coding.h:169-204.  st: 1 decoding/ok, 0 corrupt,
+  // 2 no space, 3 no block.
+  uint32_t st = exists ? 1u : 3u, want = 0, hlen = 0;
+  if (exists) {
+    const uint64_t h = view8(src);
+    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
+      const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
+      if ((b & 0x80u) == 0) {
+        want |= b << (7 * k);
+        hlen = k + 1;
+        break;
+      }
+      want |= (b & 0x7fu) << (7 * k);
+    }
+    if (hlen == 0 || want > 0x7fffffffu) st = 0;                // snappy.c:405-409
+    else if (want > cap) st = 2;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0f70);
+
+  uint32_t pos = hlen;               // next tag (stream offset)
+  uint32_t made = 0, F = 0;          // output produced / flushed
+  uint32_t in_req = 0, in_have = 0;  // input requested / landed (64-byte units)
+  uint32_t orem = 0, okind = 0, odist = 0, olp = 0;   // current op: bytes left, ...
+  bool ofar = false;
+  u32x4 fa0 = {0, 0, 0, 0}, fa1 = fa0, fa2 = fa0, fa3 = fa0;   // far-copy bytes
+  u32x4 rv0 = fa0, rv1 = fa0;                                  // refill bytes (worker)
+  const uint32_t sink = lane * kInStride + kInSink;   // own slack: no shared-address writes
+  uint32_t ra0 = sink, rm0 = sink, ra1 = sink, rm1 = sink;
+
+  for (;;) {
+    const bool active = st == 1 && !(orem == 0 && pos >= slen && F >= made);
+    if (ballot(active) == 0) break;
+
+    // ---- everything issued last trip has landed
+    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+    lwr16(s_in + ra0, rv0);
+    lwr16(s_in + rm0, rv0);
+    lwr16(s_in + ra1, rv1);
+    lwr16(s_in + rm1, rv1);
+    order();
+    in_have = in_req;
+
+    // ---- one piece of the current op (snappy.c:210-331)
+    if (st == 1 && orem > 0) {
+      const bool lit = okind == 0;
+      const uint32_t piece = orem < 64 ? orem : 64;
+      if (!lit || in_have >= olp + piece) {
+        const uint32_t dist = odist;
+        const bool overlap = !lit && dist < piece;
+        const bool pat = overlap && dist <= 8 && (dist & (dist - 1)) == 0;
+        if (overlap && !pat) {
+          // Period not dividing 16: chunk by chunk, each reading bytes the
+          // previous ones wrote (LDS program order); chunk 0 of a period
+          // < 16 is built byte by byte, later chunks copy from qq back
+          // (qq = a multiple of the period >= 16).
+          const uint32_t qq = dist >= 16 ? dist : dist * ((16 + dist - 1) / dist);
+          u32x4 p0;
+          if (dist >= 16) {
+            p0 = lrd16(ob + ((made - dist) & (kOutRing - 1)));
+          } else {
+            const u32x4 c0 = lrd16(ob + ((made - dist) & (kOutRing - 1)));
+            uint32_t w[4] = {0, 0, 0, 0};
+            uint32_t r = 0;
+#pragma clang loop unroll(disable)
+            for (uint32_t j = 0; j < 16; ++j) {
+              w[j >> 2] |= byte_of(c0, r) << (8 * (j & 3u));
+              r = r + 1 == dist ? 0 : r + 1;
+            }
+            p0 = u32x4{w[0], w[1], w[2], w[3]};
+          }
+          out_put(ob, made, p0);
+          order();
+#pragma clang loop unroll(disable)
+          for (uint32_t k = 1; 16 * k < piece; ++k) {
+            const u32x4 v = lrd16(ob + ((made + 16 * k - qq) & (kOutRing - 1)));
+            out_put(ob, made + 16 * k, v);
+            order();
+          }
+        } else {
+          u32x4 c0, c1, c2, c3;
+          if (lit) {
+            const uint8_t* sp = ib + (olp & (kInRing - 1));
+            c0 = lrd16(sp);
+            c1 = lrd16(sp + 16);
+            c2 = lrd16(sp + 32);
+            c3 = lrd16(sp + 48);
+          } else if (ofar) {
+            c0 = fa0;
+            c1 = fa1;
+            c2 = fa2;
+            c3 = fa3;
+          } else {
+            const uint8_t* sp = ob + ((made - dist) & (kOutRing - 1));
+            c0 = lrd16(sp);
+            c1 = lrd16(sp + 16);
+            c2 = lrd16(sp + 32);
+            c3 = lrd16(sp + 48);
+          }
+          // Period 1/2/4/8: the dist bytes before d as a 16-byte pattern.
+          const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
+          const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
+          const uint32_t px = dist == 1 ? w1 : (dist == 2 ? w2 : c0.x);
+          const uint32_t py = dist == 8 ? c0.y : px;
+          const u32x4 pv = {px, py, px, py};
+          out_put(ob, made, pat ? pv : c0);
+          if (piece > 16) out_put(ob, made + 16, pat ? pv : c1);
+          if (piece > 32) out_put(ob, made + 32, pat ? pv : c2);
+          if (piece > 48) out_put(ob, made + 48, pat ? pv : c3);
+        }
+        made += piece;
+        orem -= piece;
+        if (lit) olp += piece;
+      }
+    }
+    order();
+
+    // ---- flush: 128 finished bytes, or the block's last bytes once the
+    // stream is consumed (snappy.c:337: it must end exactly at want).
+    if (st == 1 && orem == 0 && pos >= slen && made != want) st = 0;
+    const bool fin = st == 1 && orem == 0 && pos >= slen;
+    const uint32_t fcnt = made - F >= kFlush ? kFlush : (fin ? made - F : 0u);
+    {
+      const bool need = st == 1 && fcnt > 0;
+      const uint64_t m = ballot(need);
+      const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      const uint32_t total = uni((uint32_t)__builtin_popcountll(m));
+      if (need) {
+        const uint64_t dp = reinterpret_cast<uint64_t>(dst);
+        s_job[j] = RingJob{lane, F, fcnt, (uint32_t)dp, (uint32_t)(dp >> 32), 0, 0, 0};
+      }
+      order();
+#pragma clang loop unroll(disable)
+      for (uint32_t base = 0; base < total; base += 8) {
+        const uint32_t jj = base + (lane >> 3), w = lane & 7u;
+        if (jj < total) {
+          const RingJob jb = s_job[jj];
+          if (16 * w < jb.cnt) {
+            const u32x4 v = lrd16(s_out + jb.lane * kOutStride + 16 +
+                                  ((jb.off + 16 * w) & (kOutRing - 1)));
+            const gptr<uint8_t> g =
+                (gptr<uint8_t>)(((uint64_t)jb.phi << 32) | jb.plo) + jb.off + 16 * w;
+            if (16 * w + 16 <= jb.cnt) st16(g, v);
+            else st_exact(g, v, jb.cnt - 16 * w);
+          }
+        }
+      }
+      order();
+      if (need) F += fcnt;
+    }
+
+    // ---- parse the next tag (its bytes are in the window)
+    if (st == 1 && orem == 0 && pos < slen) {
+      const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
+      if (in_have >= need_to) {
+        const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
+        if (t.bad) {
+          st = 0;
+        } else {
+          orem = t.len;
+          okind = t.kind == 0 ? 0u : 1u;
+          odist = t.dist;
+          olp = pos + t.hl;
+          pos = t.next;
+          ofar = okind != 0 && odist > kNear;
+          if (ofar) {
+            // Flushed already: it ends <= made - kNear + 64 < F.
+            const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
+            fa0 = ld16(sp);
+            if (orem > 16) fa1 = ld16(sp + 16);
+            if (orem > 32) fa2 = ld16(sp + 32);
+            if (orem > 48) fa3 = ld16(sp + 48);
+          }
+        }
+      }
+    }
+
+    // ---- refill requests: the next 64 input bytes, once the 64 they
+    // overwrite in the ring are consumed.  4 lanes per request, <= 32 a trip.
+    {
+      const uint32_t cons = (orem > 0 && okind == 0) ? olp : pos;
+      const bool need = st == 1 && in_req < slen && in_req <= cons + 64;
+      const uint64_t m = ballot(need);
+      const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      const uint32_t total = uni((uint32_t)__builtin_popcountll(m));
+      if (need && j < 32) {
+        const uint64_t sp = reinterpret_cast<uint64_t>(src);
+        s_job[j] = RingJob{lane, in_req, slen, (uint32_t)sp, (uint32_t)(sp >> 32), 0, 0, 0};
+      }
+      order();
+      ra0 = rm0 = ra1 = rm1 = sink;
+      const uint32_t w = lane & 3u;
+      if ((lane >> 2) < total) {
+        const RingJob jb = s_job[lane >> 2];
+        const uint32_t o = jb.off + 16 * w;
+        const gptr<const uint8_t> g = (gptr<const uint8_t>)(((uint64_t)jb.phi << 32) | jb.plo);
+        if (o < jb.cnt) rv0 = ld16(g + o);
+        const uint32_t r = o & (kInRing - 1);
+        ra0 = jb.lane * kInStride + r;
+        rm0 = r < 64 ? ra0 + kInRing : sink;
+      }
+      if (16 + (lane >> 2) < total) {
+        const RingJob jb = s_job[16 + (lane >> 2)];
+        const uint32_t o = jb.off + 16 * w;
+        const gptr<const uint8_t> g = (gptr<const uint8_t>)(((uint64_t)jb.phi << 32) | jb.plo);
+        if (o < jb.cnt) rv1 = ld16(g + o);
+        const uint32_t r = o & (kInRing - 1);
+        ra1 = jb.lane * kInStride + r;
+        rm1 = r < 64 ? ra1 + kInRing : sink;
+      }
+      order();
+      if (need && j < 32) in_req += 64;
+    }
+  }
+
+  if (exists) {
+    status[i] = (uint8_t)st;
+    out_len[i] = st == 1 ? want : 0;
+  }
+}
+
+hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
+  const uint32_t grid = (a.n + 63) / 64;
+  hipLaunchKernelGGL(decode_ring_kernel, dim3(grid), dim3(64), 0, s, a.in, a.in_off, a.in_len,
+                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+  return hipGetLastError();
+}
+
 constexpr uint32_t kDecCap0 = 4608;    // fillseq "4 KiB" blocks (max 4208 B)
 constexpr uint32_t kDecCap1 = 16896;   // 16 KiB class
 constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoot)
@@ -737,13 +1034,14 @@ static hipError_t launch_decode_lane(const DecodeArgs& a, hipStream_t s) {
 
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const char* force = getenv("LGS_DECODE_KERNEL");   // "wave" | "lane64" | "lane32"
+  const char* force = getenv("LGS_DECODE_KERNEL");   // "ring" | "wave" | "lane64" | ...
   if (force) {
+    if (!strcmp(force, "ring")) return launch_decode_ring(a, s);
     if (!strcmp(force, "lane64")) return launch_decode_lane<64>(a, s);
     if (!strcmp(force, "lane32")) return launch_decode_lane<32>(a, s);
     if (!strcmp(force, "lane16")) return launch_decode_lane<16>(a, s);
-  } else if (a.n >= kLaneMinBlocks && max_out <= kDecCap1) {
-    return launch_decode_lane<64>(a, s);
+  } else if (a.n >= kLaneMinBlocks) {
+    return launch_decode_ring(a, s);
   }
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 5632, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 19968, 1>(a, s);

@@ -197,7 +197,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lane64", "lane32"])
+@pytest.mark.parametrize("kernel", ["wave", "lane64", "lane32", "ring"])
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, monkeypatch):
     # Every decode kernel (forced through LGS_DECODE_KERNEL) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -224,7 +224,7 @@ def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
-    for kernel in ("lane64", "lane32", "wave"):
+    for kernel in ("ring", "lane64", "lane32", "wave"):
         monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
         out = batch.decode_slots(c.len)
         st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
@@ -254,3 +254,39 @@ def test_encode_kernel_variants(gpu, vectors, digests, kernel, monkeypatch):
     batch.encode(raw, comp)
     torch.cuda.synchronize()
     assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"]), kernel
+
+
+def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, monkeypatch):
+    # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
+    # literals streamed through the input window, far copies) and on output
+    # slots at odd offsets (flushes that are not line aligned, byte-exact
+    # block ends next to the neighbouring block).
+    import torch
+    from lcdb_amd import batch
+    monkeypatch.setenv("LGS_DECODE_KERNEL", "ring")
+    d = digests["C3_mixed"]
+    c = corpus.mixed()
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    out = batch.decode_slots(c.len)
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    batch.decode(comp, out, st)
+    torch.cuda.synchronize()
+    assert bool((st == 1).all())
+    assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"])
+    # odd slots, packed back to back (no slack between blocks)
+    lens = c.len.astype(np.int64)
+    off = np.zeros(c.n, dtype=np.int64)
+    off[1:] = np.cumsum(lens[:-1])
+    off += 3
+    out2 = batch.Slots(torch.zeros(int(lens.sum()) + 3 + 16, dtype=torch.uint8, device="cuda"),
+                       torch.from_numpy(off).cuda(), torch.zeros(c.n, dtype=torch.int32, device="cuda"),
+                       torch.from_numpy(lens.astype(np.int32)).cuda(), int(lens.max()))
+    st.zero_()
+    batch.decode(comp, out2, st)
+    torch.cuda.synchronize()
+    assert bool((st == 1).all())
+    host = out2.buf.cpu().numpy()
+    ref = np.concatenate([np.frombuffer(c.block(k), dtype=np.uint8) for k in range(c.n)])
+    assert np.array_equal(host[3:3 + len(ref)], ref)
