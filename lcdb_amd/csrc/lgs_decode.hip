@@ -820,17 +820,10 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     const bool active = st == 1 && !(orem == 0 && pos >= slen && F >= made);
     if (ballot(active) == 0) break;
 
-    // ---- everything issued last trip has landed
-    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
-    lwr16(s_in + ra0, rv0);
-    lwr16(s_in + rm0, rv0);
-    lwr16(s_in + ra1, rv1);
-    lwr16(s_in + rm1, rv1);
-    order();
-    in_have = in_req;
-
-    // ---- one piece of the current op (snappy.c:210-331)
-    if (st == 1 && orem > 0) {
+    // ---- one piece of the current op (snappy.c:210-331) for every lane
+    // whose bytes are in LDS (literal from the window, copy from the ring);
+    // this runs before the wait, so last trip's loads land meanwhile.
+    if (st == 1 && orem > 0 && !ofar) {
       const bool lit = okind == 0;
       const uint32_t piece = orem < 64 ? orem : 64;
       if (!lit || in_have >= olp + piece) {
@@ -873,11 +866,6 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
             c1 = lrd16(sp + 16);
             c2 = lrd16(sp + 32);
             c3 = lrd16(sp + 48);
-          } else if (ofar) {
-            c0 = fa0;
-            c1 = fa1;
-            c2 = fa2;
-            c3 = fa3;
           } else {
             const uint8_t* sp = ob + ((made - dist) & (kOutRing - 1));
             c0 = lrd16(sp);
@@ -902,6 +890,25 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       }
     }
     order();
+
+    // ---- everything issued last trip has landed: far-copy pieces (never
+    // overlapping, <= 64 bytes), then the input refills.
+    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+    if (st == 1 && orem > 0 && ofar) {
+      out_put(ob, made, fa0);
+      if (orem > 16) out_put(ob, made + 16, fa1);
+      if (orem > 32) out_put(ob, made + 32, fa2);
+      if (orem > 48) out_put(ob, made + 48, fa3);
+      made += orem;
+      orem = 0;
+      ofar = false;
+    }
+    lwr16(s_in + ra0, rv0);
+    lwr16(s_in + rm0, rv0);
+    lwr16(s_in + ra1, rv1);
+    lwr16(s_in + rm1, rv1);
+    order();
+    in_have = in_req;
 
     // ---- flush: 128 finished bytes, or the block's last bytes once the
     // stream is consumed (snappy.c:337: it must end exactly at want).

@@ -20,9 +20,9 @@
 //  * match extension (snappy.c:163-164): 64 byte-compares per step, the
 //    first mismatch found by ballot.
 //  * post-copy re-probe, including lcdb's 64-bit compare (snappy.c:172-186):
-//    scalar.
-//  * emission (snappy.c:53-102): header bytes and literal bytes written by
-//    lanes straight to the output.
+//    the same work on every lane (VALU + LDS broadcast), off the scalar unit.
+//  * emission (snappy.c:53-102): the literal and the copy tags that follow it
+//    in one lane-parallel pass, stored straight to the output.
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
@@ -188,15 +188,19 @@ struct Seq {
 constexpr uint32_t kSink = kTableCap;
 
 // Encode one chunk x[0..n), 17 <= n <= 65536, held in LDS.  `tab` is the
-// u16 hash table, `lid` a u8 lane-id scratch (both with a sink slot).  Writes to
-// o, returns bytes written.  Mirrors snappy.c:104-195 step for step.
+// u16 hash table (with a sink slot).  Writes to o, returns bytes written.
+// Mirrors snappy.c:104-195 step for step.
 //
 // Literal-search batches.  Probe index pi = 63 - lane (lane 63 takes the
-// earliest probe).  Each valid probe scatters pi into lid[hash]; the LDS
+// earliest probe).  Each lane first reads its candidate from the table;
+// then each valid probe scatters pi into tab[hash] itself (the table
+// doubles as the lane-id scratch: no second 2048-entry array, so more waves
+// fit in LDS) and every lane writes its candidate back before the commit
+// write.  The LDS
 // keeps one writer per address (on gfx950 the highest lane, i.e. the
 // earliest probe -- but nothing below depends on which).  A probe that reads
 // back another pi ("loser") shares its hash with another probe of the
-// batch.  Losers then scatter their pi into lid again (winners do not), which
+// batch.  Losers then scatter their pi again (winners do not), which
 // singles out the second member of each hash group.  When every loser sees its group's
 // winners before itself (checked with a ballot), the winner is the
 // earliest probe of the group and:
@@ -211,7 +215,7 @@ constexpr uint32_t kSink = kTableCap;
 // A found match is extended, then its literal and copy are emitted in one
 // pass (emit_seq), then lcdb's immediate re-probe runs (snappy.c:172-186)
 // as identical work on every lane.
-__device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, uint8_t* lid,
+__device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
                                  const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
   const uint32_t pi = 63 - lane;                      // probe index in the batch
@@ -260,19 +264,20 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
     // lane-id rounds below: issue them first so their LDS latency overlaps.
     const uint32_t ct = tab[hh];                                  // snappy.c:146
     uint32_t yv = lds_ld32(x, valid ? ct : 0);
-    lid[hh] = (uint8_t)pi;
     order();
-    const uint32_t w1 = lid[hh];
+    tab[hh] = (uint16_t)pi;
+    order();
+    const uint32_t w1 = tab[hh];
     const bool loser = valid & (w1 != pi);
     const uint64_t lmask = ballot(loser);
     uint32_t ncut = 64, w2 = 0xffu;
     uint64_t second = 0;                                          // lanes comparing to their group's first
     if (lmask) {
-      // Round two reuses lid: only losers write, so a group without a
-      // loser still reads its winner back (w2 == w1).
-      lid[loser ? hh : kSink] = (uint8_t)pi;
+      // Round two: only losers write, so a group without a loser still
+      // reads its winner back (w2 == w1).
+      tab[loser ? hh : kSink] = (uint16_t)pi;
       order();
-      const uint32_t r2 = lid[hh];
+      const uint32_t r2 = tab[hh];
       w2 = r2 == w1 ? 0xffu : r2;                                // winners: 2nd member or none
       const uint32_t wmax = w1 > r2 ? w1 : r2;
       if (ballot(loser & (wmax > pi))) {                          // a group out of order
@@ -292,6 +297,8 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab, ui
     const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
     // snappy.c:148; a group's first probe defers to its second if both commit.
     const bool shadowed = (second != 0) & !loser & (w2 < ncommit);
+    tab[hh] = (uint16_t)ct;                                       // undo the scatters
+    order();
     tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
     order();
 
@@ -378,7 +385,6 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
   __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap + 8];   // + sink
-  __shared__ __attribute__((aligned(16))) uint8_t s_lid[WAVES][kTableCap + 16];      // + sink
 
   // Per-wave scalars go through v_readfirstlane so hipcc keeps the control
   // flow on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
@@ -421,7 +427,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* x = &s_in[wv][sh];
     order();
     if (clen >= kMinBlock) {
-      op = encode_chunk(x, clen, &s_tab[wv][0], &s_lid[wv][0], o, op, off0, off1);
+      op = encode_chunk(x, clen, &s_tab[wv][0], o, op, off0, off1);
     } else {
       op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
