@@ -231,19 +231,31 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
 
   uint32_t op = op0;     // output cursor (byte offset in the slot)
   uint32_t lit = 0;      // first byte not yet emitted (snappy.c:111 "emit")
-  uint32_t start = 1;    // where the current literal search began (snappy.c:112)
-  uint32_t k = 0;        // probes of this search already done
+  uint32_t at = 0;       // end of the last copy
+  uint32_t start = 1;    // first probe position of the current search (snappy.c:112)
+  uint32_t kv = 2;       // virtual probe index of this batch's first lane
 
-  // One loop with one exit: each trip is one 64-probe batch of a literal
-  // search and, when the batch finds a match, the copies that follow it.
-  // (Loops with several exits get a selector variable and compare chains
-  // from the compiler's loop-exit unification: scalar work on every trip.)
+  // Each batch takes 64 consecutive probes of a virtual sequence:
+  //   v = 0: A, position at-1 -- the re-probe's first insert (snappy.c:172-175),
+  //   v = 1: B, position at   -- its insert and 64-bit compare (snappy.c:177-182),
+  //   v >= 2: search probe v-2 from start = at+1 (snappy.c:133-154).
+  // A and B exist only after a copy (a chunk's first search starts at
+  // v = 2).  They are ordinary probes to the collision logic, which gives
+  // the serial order's table semantics (B's candidate is at-1 when A and B
+  // share a hash); A never matches, and B's match is the re-match of
+  // snappy.c:182.  Folding the re-probe into the batch removes its three
+  // dependent LDS round trips from every copy.
+  //
+  // One loop with one exit: each trip is one batch and, if it finds a match,
+  // the copy that follows.  (Loops with several exits get a selector
+  // variable and compare chains from the compiler's loop-exit unification:
+  // scalar work on every trip.)
   for (;;) {
-    // ---- literal search (snappy.c:133-154), probes k .. k+63 of the search.
-    uint32_t o0 = off0, o1 = off1;
+    const uint32_t v = kv + pi;
+    uint32_t o0 = off0, o1 = off1;                  // search probe pi - 2 (kv == 0)
     bool in_tab = true;
-    if (k != 0) {                                   // long search: later schedule
-      const uint32_t kk = k + pi;
+    if (kv != 0) {                                  // other batches: later schedule
+      const uint32_t kk = v - 2;                    // (wraps for v < 2: unused)
       in_tab = kk < kProbeTab;
       const uint32_t kc = in_tab ? kk : kProbeTab - 1;
       o0 = kProbe.off[kc];
@@ -254,15 +266,19 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
       // until the previous copy's bytes had reached memory.
       __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
     }
-    const bool valid = in_tab && start + o1 <= last;              // snappy.c:143
+    const bool isA = v == 0, isB = v == 1;
+    const bool valid = v < 2 || (in_tab && start + o1 <= last);  // snappy.c:143
     const uint64_t vmask = ballot(valid);
-    const uint32_t p = valid ? start + o0 : 0;
+    const uint32_t ps = valid ? start + o0 : 0;
+    const uint32_t pab = isA ? at - 1 : at;
+    const uint32_t p = v < 2 ? pab : ps;
 
-    const uint32_t xv = lds_ld32(x, p);
+    const uint64_t xw = lds_ld64(x, p);                           // bytes p .. p+7
+    const uint32_t xv = (uint32_t)xw;
     const uint32_t hh = valid ? hash32(xv, shift) : kSink;
     // The table read and the candidate's bytes do not depend on the
     // lane-id rounds below: issue them first so their LDS latency overlaps.
-    const uint32_t ct = tab[hh];                                  // snappy.c:146
+    const uint32_t ct = tab[hh];                                  // snappy.c:146, :177
     uint32_t yv = lds_ld32(x, valid ? ct : 0);
     order();
     tab[hh] = (uint16_t)pi;
@@ -293,9 +309,15 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
         yv = loser ? xfirst : yv;
       }
     }
-    const uint64_t mm = ballot((pi < ncut) & (xv == yv)) & vmask;     // snappy.c:152
+    // snappy.c:152; A never matches; B is lcdb's 64-bit compare (snappy.c:182):
+    // bytes at..at+6 against a zero-extended 4-byte load.
+    const bool eq = xv == yv;
+    const bool hi0 = ((uint32_t)(xw >> 32) & 0xffffffu) == 0;
+    const bool mt = isA ? false : (isB ? (eq & hi0) : eq);
+    const uint64_t mm = ballot((pi < ncut) & mt) & vmask;
     const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
-    // snappy.c:148; a group's first probe defers to its second if both commit.
+    // snappy.c:148, :175, :179; a group's first probe defers to its second
+    // if both commit.
     const bool shadowed = (second != 0) & !loser & (w2 < ncommit);
     tab[hh] = (uint16_t)ct;                                       // undo the scatters
     order();
@@ -305,67 +327,47 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
     bool done;
     if (mm) {
       const uint32_t src = 63 - (ncommit - 1);
-      uint32_t at = lane_val(p, src);
-      uint32_t ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
-                                           : lane_val(ct, src);
-      // ---- copies, with lcdb's immediate re-match (snappy.c:158-187).
-      bool again;
-      do {
-        const uint32_t base = at;
-        uint32_t r = ref + 4;
-        at += 4;
+      at = lane_val(p, src);
+      const uint32_t ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
+                                                 : lane_val(ct, src);
+      // ---- the copy (snappy.c:158-169)
+      const uint32_t base = at;
+      uint32_t r = ref + 4;
+      at += 4;
 #pragma clang loop unroll(disable)
-        for (;;) {                                                // snappy.c:163-164
-          const uint32_t q = at + lane;
-          // Clamped unconditional reads (q < n implies r + lane < n).
-          const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
-          const bool same = (q < n) & (x[ra] == x[qa]);
-          const uint64_t diff = ballot(!same);
-          if (diff) {
-            at += (uint32_t)__builtin_ctzll(diff);
-            break;
-          }
-          at += kWave;
-          r += kWave;
+      for (;;) {                                                  // snappy.c:163-164
+        const uint32_t q = at + lane;
+        // Clamped unconditional reads (q < n implies r + lane < n).
+        const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
+        const bool same = (q < n) & (x[ra] == x[qa]);
+        const uint64_t diff = ballot(!same);
+        if (diff) {
+          at += (uint32_t)__builtin_ctzll(diff);
+          break;
         }
+        at += kWave;
+        r += kWave;
+      }
 
-        // snappy.c:156 + 166: the literal before the copy, then the copy
-        // (copies of 68+ bytes, rare, get their tags from emit_copy).
-        const uint32_t clen = at - base, dist = base - ref;
-        const bool longc = clen >= 68;
-        const Seq sq(lit, base - lit, longc ? 0u : dist, longc ? 0u : clen);
-        sq.pass(o, op, x, n, 0);
-
-        done = at >= last;                                        // snappy.c:169
-        // snappy.c:172-180, as identical work on every lane (VALU + LDS
-        // broadcast), run even when `done` (the table is dead then, and the
-        // reads stay inside the LDS pad) so that it has no branch around it
-        // and the scheduler can overlap it with the emission pass above.
-        // Every lane does the same work, so single-thread program order is
-        // the real order: no order() barriers.  lcdb's 64-bit compare
-        // (snappy.c:182): bytes at..at+6 against a zero-extended 4-byte load.
-        const uint32_t va = vec(at);
-        const uint64_t w = lds_ld64(x, va - 1);
-        const uint32_t h1 = hash32((uint32_t)w, shift), h2 = hash32((uint32_t)(w >> 8), shift);
-        tab[h1] = (uint16_t)(va - 1);
-        const uint32_t c = tab[h2];
-        tab[h2] = (uint16_t)va;
-        const bool hit = ballot((w >> 8) == (uint64_t)lds_ld32(x, c)) != 0;
-        again = !done && hit;
-        ref = uni(c);
-
-        sq.rest(o, op, x, n);
-        op += sq.total;
-        if (longc) op += emit_copy(o, op, dist, clen);
-        lit = at;
-      } while (again);
+      // snappy.c:156 + 166: the literal before the copy (empty after a
+      // re-match), then the copy (copies of 68+ bytes, rare, get their tags
+      // from emit_copy).
+      const uint32_t clen = at - base, dist = base - ref;
+      const bool longc = clen >= 68;
+      const Seq sq(lit, base - lit, longc ? 0u : dist, longc ? 0u : clen);
+      sq.pass(o, op, x, n, 0);
+      sq.rest(o, op, x, n);
+      op += sq.total;
+      if (longc) op += emit_copy(o, op, dist, clen);
+      lit = at;
+      done = at >= last;                                          // snappy.c:169
       start = at + 1;                                             // snappy.c:184-185
-      k = 0;
+      kv = 0;
     } else {
       // No match in this batch: the search ends if a probe before the cut
       // was past the limit, else continues after the cut.
       done = (uint32_t)__builtin_popcountll(vmask) < ncut;
-      k += ncut;
+      kv += ncut;
     }
     if (done) break;
   }
@@ -393,8 +395,10 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   if (slot >= n) return;
   const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
-  // Probe offsets of the first 64 probes of a search, kept in registers.
-  const uint32_t off0 = kProbe.off[63 - lane], off1 = kProbe.off[64 - lane];
+  // Probe offsets of search probes pi - 2 (the batch right after a copy,
+  // whose lanes pi = 0, 1 are the re-probe), kept in registers.
+  const uint32_t pk = (63 - lane) >= 2 ? 61 - lane : 0;
+  const uint32_t off0 = kProbe.off[pk], off1 = kProbe.off[pk + 1];
   // Settle these loads now: otherwise the compiler cannot prove them done
   // inside the batch loop and waits vmcnt(0) there -- on every batch, behind
   // every pending output store.
