@@ -215,7 +215,7 @@ constexpr uint32_t kSink = kTableCap;
 // A found match is extended, then its literal and copy are emitted in one
 // pass (emit_seq), then lcdb's immediate re-probe runs (snappy.c:172-186)
 // as identical work on every lane.
-__device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
+__device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
                                  const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
   const uint32_t pi = 63 - lane;                      // probe index in the batch
@@ -234,6 +234,8 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
   uint32_t at = 0;       // end of the last copy
   uint32_t start = 1;    // first probe position of the current search (snappy.c:112)
   uint32_t kv = 2;       // virtual probe index of this batch's first lane
+  // The last copy's emission, deferred into the next batch (below).
+  uint32_t e_lit = 0, e_L = 0, e_D = 0, e_C = 0, e_longlen = 0;
 
   // Each batch takes 64 consecutive probes of a virtual sequence:
   //   v = 0: A, position at-1 -- the re-probe's first insert (snappy.c:172-175),
@@ -266,6 +268,13 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
       // until the previous copy's bytes had reached memory.
       __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
     }
+    // The previous copy's literal + tags (snappy.c:156, :166), emitted here
+    // as straight-line code in the batch's first block, so that it fills the
+    // batch's LDS waits instead of lengthening the copy -> batch chain.
+    // (Nothing pending: a zero-length sequence, every store dropped.)
+    const Seq sq(e_lit, e_L, e_D, e_C);
+    sq.pass(o, op, x, n, 0);
+
     const bool isA = v == 0, isB = v == 1;
     const bool valid = v < 2 || (in_tab && start + o1 <= last);  // snappy.c:143
     const uint64_t vmask = ballot(valid);
@@ -323,6 +332,10 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
     order();
     tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
     order();
+    sq.rest(o, op, x, n);                                         // rare: > 64 bytes
+    op += sq.total;
+    if (e_longlen) op += emit_copy(o, op, e_D, e_longlen);        // rare: 68+ byte copy
+    e_L = e_C = e_longlen = 0;
 
     bool done;
     if (mm) {
@@ -350,15 +363,15 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
       }
 
       // snappy.c:156 + 166: the literal before the copy (empty after a
-      // re-match), then the copy (copies of 68+ bytes, rare, get their tags
-      // from emit_copy).
+      // re-match), then the copy -- emitted during the next batch (copies
+      // of 68+ bytes, rare, get their tags from emit_copy).
       const uint32_t clen = at - base, dist = base - ref;
       const bool longc = clen >= 68;
-      const Seq sq(lit, base - lit, longc ? 0u : dist, longc ? 0u : clen);
-      sq.pass(o, op, x, n, 0);
-      sq.rest(o, op, x, n);
-      op += sq.total;
-      if (longc) op += emit_copy(o, op, dist, clen);
+      e_lit = lit;
+      e_L = base - lit;
+      e_D = dist;
+      e_C = longc ? 0u : clen;
+      e_longlen = longc ? clen : 0u;
       lit = at;
       done = at >= last;                                          // snappy.c:169
       start = at + 1;                                             // snappy.c:184-185
@@ -370,6 +383,13 @@ __device__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
       kv += ncut;
     }
     if (done) break;
+  }
+  {                                                               // the last copy's emission
+    const Seq sq(e_lit, e_L, e_D, e_C);
+    sq.pass(o, op, x, n, 0);
+    sq.rest(o, op, x, n);
+    op += sq.total;
+    if (e_longlen) op += emit_copy(o, op, e_D, e_longlen);
   }
 
   if (lit < n) op += emit_literal(o, op, x, lit, n - lit);         // snappy.c:190-192
