@@ -105,6 +105,78 @@ int lgs_decode_batch_host(const uint8_t *in, const uint64_t *in_off,
                           const uint64_t *out_off, const uint32_t *out_cap,
                           uint32_t *out_len, uint8_t *status, uint32_t n);
 
+/* ---- SSTable block framing ----
+ *
+ * lcdb frames every table block as  contents | type (1 byte) | masked
+ * crc32c of contents+type (fixed32)  (table_builder.c:123-153), and reads a
+ * block back through format.c:162-270.  These calls do both for many blocks
+ * per launch, byte-identical to the reference doing them one at a time. */
+
+#define LGS_NO_COMPRESSION      0   /* enum ldb_compression (options.h)       */
+#define LGS_SNAPPY_COMPRESSION  1
+#define LGS_TRAILER_SIZE        5   /* LDB_TRAILER_SIZE (format.h:34)         */
+
+/* Further per-block read statuses (besides LGS_ST_CORRUPT/OK/NOSPACE). */
+#define LGS_ST_IOERR    3   /* truncated block read -> LDB_IOERR (format.c:195-198)     */
+#define LGS_ST_BADCRC   4   /* checksum mismatch -> LDB_CORRUPTION (format.c:203-211)   */
+#define LGS_ST_BADTYPE  5   /* bad block type -> LDB_CORRUPTION (format.c:263-267)      */
+
+/* Row 1.  d_crc[i] = ldb_crc32c_value(block i) (crc32c.c:1147, crc32c.h:29),
+   extended over the byte d_type[i] when d_type != NULL (table_builder.c:139-
+   140), then ldb_crc32c_mask'ed (crc32c.h:46-50) when masked != 0.  With a
+   type and masked = 1 this is the trailer's crc field.  Asynchronous. */
+int lgs_crc32c_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
+                         const uint32_t *d_in_len, const uint8_t *d_type,
+                         int masked, uint32_t *d_crc, uint32_t n, void *stream);
+
+/* Row 2.  n finished data blocks (ldb_blockgen_finish output, raw bytes)
+   written as ldb_tablegen_write_block writes them (table_builder.c:155-213):
+   snappy-encoded when compression = LGS_SNAPPY_COMPRESSION and that saves
+   more than 12.5 % (:190), else raw; each followed by its trailer; block i at
+   file offset handle_off[i] with handle_size[i] content bytes (:128-129);
+   the first block at offset `base`.  d_file[j] receives file offset base + j;
+   *d_end = base + bytes written.  d_file needs sum(raw_len) + 5n bytes.
+   raw_total = sum of the raw lengths (sizes the scratch);
+   d_scratch: lgs_table_write_scratch(n, raw_total) device bytes.  Inputs
+   must stay readable 16 bytes past each block.  Asynchronous. */
+size_t lgs_table_write_scratch(uint32_t n, uint64_t raw_total);
+int lgs_table_write_dev(const uint8_t *d_raw, const uint64_t *d_raw_off,
+                        const uint32_t *d_raw_len, uint32_t n, uint32_t max_raw_len,
+                        uint64_t raw_total, int compression, uint64_t base,
+                        uint8_t *d_file, uint64_t *d_handle_off,
+                        uint64_t *d_handle_size, uint64_t *d_end,
+                        void *d_scratch, size_t scratch_bytes, void *stream);
+/* Host buffers; returns when file/handles/end are written.  file_cap: room
+   in `file` (sum(raw_len) + 5n always suffices). */
+int lgs_table_write_host(const uint8_t *raw, const uint64_t *raw_off,
+                         const uint32_t *raw_len, uint32_t n, int compression,
+                         uint64_t base, uint8_t *file, size_t file_cap,
+                         uint64_t *handle_off, uint64_t *handle_size,
+                         uint64_t *end);
+
+/* Row 3.  ldb_read_block (format.c:162-270) for n block handles of one
+   table image (d_file[0 .. file_len) = file offsets 0 ..): truncation check,
+   trailer check when verify_checksums, then raw copy or snappy decode into
+   d_out + d_out_off[i] (capacity d_out_cap[i]; the decoded size of a snappy
+   block is its varint32 header, ldb_snappy_decode_size).  d_status[i] =
+   LGS_ST_OK or the reason the reference fails; d_out_len[i] = contents
+   length when ok.  d_file must stay readable 16 bytes past file_len.
+   d_scratch: lgs_table_read_scratch(n) device bytes.  Asynchronous. */
+size_t lgs_table_read_scratch(uint32_t n);
+int lgs_table_read_dev(const uint8_t *d_file, uint64_t file_len,
+                       const uint64_t *d_handle_off, const uint64_t *d_handle_size,
+                       uint32_t n, int verify_checksums, uint8_t *d_out,
+                       const uint64_t *d_out_off, const uint32_t *d_out_cap,
+                       uint32_t max_out_cap, uint32_t *d_out_len, uint8_t *d_status,
+                       void *d_scratch, size_t scratch_bytes, void *stream);
+/* Host buffers (e.g. an mmap'd .ldb); only the handles' byte ranges are
+   uploaded.  Returns when out/out_len/status are written. */
+int lgs_table_read_host(const uint8_t *file, uint64_t file_len,
+                        const uint64_t *handle_off, const uint64_t *handle_size,
+                        uint32_t n, int verify_checksums, uint8_t *out,
+                        const uint64_t *out_off, const uint32_t *out_cap,
+                        uint32_t *out_len, uint8_t *status);
+
 /* Devices and diagnostics. */
 int lgs_device_count(void);
 int lgs_set_device(int device);  /* device used by the calling thread */

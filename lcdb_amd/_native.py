@@ -12,6 +12,9 @@ from .build import LIB
 
 LGS_OK = 0
 LGS_ST_CORRUPT, LGS_ST_OK, LGS_ST_NOSPACE = 0, 1, 2
+LGS_ST_IOERR, LGS_ST_BADCRC, LGS_ST_BADTYPE = 3, 4, 5
+LGS_NO_COMPRESSION, LGS_SNAPPY_COMPRESSION = 0, 1
+LGS_TRAILER_SIZE = 5
 
 _u8p = C.POINTER(C.c_uint8)
 _vp = C.c_void_p
@@ -27,6 +30,17 @@ _SIGS = {
                                        C.c_uint32, _vp]),
     "lgs_encode_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32]),
     "lgs_decode_batch_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32]),
+    "lgs_crc32c_batch_dev": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, _vp, C.c_uint32, _vp]),
+    "lgs_table_write_scratch": (C.c_size_t, [C.c_uint32, C.c_uint64]),
+    "lgs_table_write_dev": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int,
+                                      C.c_uint64, _vp, _vp, _vp, _vp, _vp, C.c_size_t, _vp]),
+    "lgs_table_write_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, C.c_int, C.c_uint64, _vp,
+                                       C.c_size_t, _vp, _vp, _vp]),
+    "lgs_table_read_scratch": (C.c_size_t, [C.c_uint32]),
+    "lgs_table_read_dev": (C.c_int, [_vp, C.c_uint64, _vp, _vp, C.c_uint32, C.c_int, _vp, _vp,
+                                     _vp, C.c_uint32, _vp, _vp, _vp, C.c_size_t, _vp]),
+    "lgs_table_read_host": (C.c_int, [_vp, C.c_uint64, _vp, _vp, C.c_uint32, C.c_int, _vp, _vp,
+                                      _vp, _vp, _vp]),
     "lgs_device_count": (C.c_int, []),
     "lgs_set_device": (C.c_int, [C.c_int]),
     "lgs_last_error": (C.c_char_p, []),

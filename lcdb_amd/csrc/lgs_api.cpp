@@ -454,6 +454,277 @@ int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   return LGS_OK;
 }
 
+// ---- SSTable block framing (kernels: lgs_table.hip) ----
+
+int lgs_crc32c_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                         const uint8_t* d_type, int masked, uint32_t* d_crc, uint32_t n,
+                         void* stream) {
+  if (n == 0) return LGS_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_crc) return fail(LGS_EINVAL, "NULL argument");
+  LGS_HIP(launch_crc(d_in, d_in_off, d_in_len, d_type, masked, d_crc, n, (hipStream_t)stream));
+  return LGS_OK;
+}
+
+namespace {
+
+// Device scratch of the write path (offsets from the scratch base).
+struct WriteScratch {
+  size_t enc_off, enc_len, part, foff, enc, total;
+  WriteScratch(uint32_t n, uint64_t raw_total) {
+    Layout L;
+    enc_off = L.take(8 * (size_t)n);
+    enc_len = L.take(4 * (size_t)n);
+    part = L.take(8 * scan_parts(n) + 8);
+    foff = L.take(8 * (size_t)n);
+    enc = L.take(48 * (size_t)n + raw_total + raw_total / 6 + 64);   // >= sum of 16-aligned bounds
+    total = L.at;
+  }
+};
+
+struct ReadScratch {
+  size_t in_off, len, off, cap, olen, st, dummy, total;
+  explicit ReadScratch(uint32_t n) {
+    Layout L;
+    in_off = L.take(8 * (size_t)n);
+    len = L.take(4 * (size_t)n);
+    off = L.take(8 * (size_t)n);
+    cap = L.take(4 * (size_t)n);
+    olen = L.take(4 * (size_t)n);
+    st = L.take((size_t)n);
+    dummy = L.take(64);
+    total = L.at;
+  }
+};
+
+int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const uint32_t* d_raw_len,
+                uint32_t n, uint32_t max_raw_len, int compression, uint64_t base, uint8_t* d_file,
+                uint64_t* d_handle_off, uint64_t* d_handle_size, uint64_t* d_end, uint8_t* scratch,
+                const WriteScratch& W, hipStream_t s) {
+  uint64_t* enc_off = (uint64_t*)(scratch + W.enc_off);
+  uint32_t* enc_len = (uint32_t*)(scratch + W.enc_len);
+  uint64_t* part = (uint64_t*)(scratch + W.part);
+  uint64_t* foff = (uint64_t*)(scratch + W.foff);
+  uint8_t* enc = scratch + W.enc;
+  const bool snappy = compression == LGS_SNAPPY_COMPRESSION;
+  if (snappy) {                       // table_builder.c:176-188, every block at once
+    LGS_HIP(launch_scan(0, d_raw_len, nullptr, part, 0, enc_off, nullptr, n, s));
+    EncodeArgs a{d_raw, d_raw_off, d_raw_len, enc, enc_off, enc_len, nullptr, nullptr, n};
+    LGS_HIP(launch_encode(a, max_raw_len, s));
+  }
+  // File offsets of the framed blocks (table_builder.c:150), then the blocks.
+  LGS_HIP(launch_scan(1, d_raw_len, snappy ? enc_len : nullptr, part, base, foff, d_end, n, s));
+  FrameArgs f{d_raw, d_raw_off, d_raw_len, enc, enc_off, snappy ? enc_len : nullptr,
+              d_file, base, foff, d_handle_off, d_handle_size, n};
+  LGS_HIP(launch_frame(f, s));
+  return LGS_OK;
+}
+
+int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* d_hoff,
+               const uint64_t* d_hsize, uint32_t n, int verify, uint8_t* d_out,
+               const uint64_t* d_out_off, const uint32_t* d_out_cap, uint32_t max_out_cap,
+               uint32_t* d_out_len, uint8_t* d_status, uint8_t* scratch, const ReadScratch& R,
+               hipStream_t s) {
+  uint64_t* dec_in_off = (uint64_t*)(scratch + R.in_off);
+  uint32_t* dec_len = (uint32_t*)(scratch + R.len);
+  uint64_t* dec_off = (uint64_t*)(scratch + R.off);
+  uint32_t* dec_cap = (uint32_t*)(scratch + R.cap);
+  uint32_t* dec_olen = (uint32_t*)(scratch + R.olen);
+  uint8_t* dec_st = scratch + R.st;
+  // The dummy slot as an offset from d_out (two's complement wrap).
+  const uint64_t dummy_off = (uint64_t)(uintptr_t)(scratch + R.dummy) - (uint64_t)(uintptr_t)d_out;
+  CheckArgs c{d_file, file_len, d_hoff, d_hsize, verify ? 1u : 0u, d_out, d_out_off, d_out_cap,
+              d_out_len, d_status, dec_in_off, dec_len, dec_off, dec_cap, dummy_off, n};
+  LGS_HIP(launch_check(c, s));
+  DecodeArgs d{d_file, dec_in_off, dec_len, d_out, dec_off, dec_cap, dec_olen, dec_st, nullptr, n};
+  LGS_HIP(launch_decode(d, max_out_cap, s));
+  LGS_HIP(launch_merge(d_status, d_out_len, dec_st, dec_olen, n, s));
+  return LGS_OK;
+}
+
+}  // namespace
+
+size_t lgs_table_write_scratch(uint32_t n, uint64_t raw_total) {
+  return WriteScratch(n, raw_total).total;
+}
+
+size_t lgs_table_read_scratch(uint32_t n) { return ReadScratch(n).total; }
+
+int lgs_table_write_dev(const uint8_t* d_raw, const uint64_t* d_raw_off,
+                        const uint32_t* d_raw_len, uint32_t n, uint32_t max_raw_len,
+                        uint64_t raw_total, int compression, uint64_t base, uint8_t* d_file,
+                        uint64_t* d_handle_off, uint64_t* d_handle_size, uint64_t* d_end,
+                        void* d_scratch, size_t scratch_bytes, void* stream) {
+  if (n == 0) return LGS_OK;
+  if (!d_raw || !d_raw_off || !d_raw_len || !d_file || !d_handle_off || !d_handle_size ||
+      !d_scratch)
+    return fail(LGS_EINVAL, "NULL argument");
+  if (compression != LGS_NO_COMPRESSION && compression != LGS_SNAPPY_COMPRESSION)
+    return fail(LGS_EINVAL, "unknown compression type %d", compression);
+  if (max_raw_len > 0x7fffffffu) return fail(LGS_EINVAL, "block of %u bytes too large", max_raw_len);
+  const WriteScratch W(n, raw_total);
+  if (scratch_bytes < W.total)
+    return fail(LGS_EINVAL, "scratch of %zu bytes, %zu needed", scratch_bytes, W.total);
+  return table_write(d_raw, d_raw_off, d_raw_len, n, max_raw_len, compression, base, d_file,
+                     d_handle_off, d_handle_size, d_end, (uint8_t*)d_scratch, W,
+                     (hipStream_t)stream);
+}
+
+int lgs_table_read_dev(const uint8_t* d_file, uint64_t file_len, const uint64_t* d_handle_off,
+                       const uint64_t* d_handle_size, uint32_t n, int verify_checksums,
+                       uint8_t* d_out, const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                       uint32_t max_out_cap, uint32_t* d_out_len, uint8_t* d_status,
+                       void* d_scratch, size_t scratch_bytes, void* stream) {
+  if (n == 0) return LGS_OK;
+  if (!d_file || !d_handle_off || !d_handle_size || !d_out || !d_out_off || !d_out_cap ||
+      !d_out_len || !d_status || !d_scratch)
+    return fail(LGS_EINVAL, "NULL argument");
+  const ReadScratch R(n);
+  if (scratch_bytes < R.total)
+    return fail(LGS_EINVAL, "scratch of %zu bytes, %zu needed", scratch_bytes, R.total);
+  return table_read(d_file, file_len, d_handle_off, d_handle_size, n, verify_checksums, d_out,
+                    d_out_off, d_out_cap, max_out_cap, d_out_len, d_status, (uint8_t*)d_scratch,
+                    R, (hipStream_t)stream);
+}
+
+int lgs_table_write_host(const uint8_t* raw, const uint64_t* raw_off, const uint32_t* raw_len,
+                         uint32_t n, int compression, uint64_t base, uint8_t* file,
+                         size_t file_cap, uint64_t* handle_off, uint64_t* handle_size,
+                         uint64_t* end) {
+  if (!end) return fail(LGS_EINVAL, "NULL argument");
+  if (n == 0) {
+    *end = base;
+    return LGS_OK;
+  }
+  if (!raw || !raw_off || !raw_len || !file || !handle_off || !handle_size)
+    return fail(LGS_EINVAL, "NULL argument");
+  if (compression != LGS_NO_COMPRESSION && compression != LGS_SNAPPY_COMPRESSION)
+    return fail(LGS_EINVAL, "unknown compression type %d", compression);
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  size_t in_total = 0, file_max = 0;
+  uint32_t max_in = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (raw_len[i] > 0x7fffffffu) return fail(LGS_EINVAL, "block %u too large", i);
+    in_total += align_up(raw_len[i], 16);
+    file_max += (size_t)raw_len[i] + LGS_TRAILER_SIZE;
+    if (raw_len[i] > max_in) max_in = raw_len[i];
+  }
+  const WriteScratch W(n, in_total);
+  Layout L;  // upload | download | device-only
+  const size_t o_in = L.take(in_total + 16);
+  const size_t o_ioff = L.take(8 * (size_t)n);
+  const size_t o_ilen = L.take(4 * (size_t)n);
+  const size_t up_end = L.at;
+  const size_t o_hoff = L.take(8 * (size_t)n);
+  const size_t o_hsize = L.take(8 * (size_t)n);
+  const size_t o_end = L.take(8);
+  const size_t o_file = L.take(file_max + 16);
+  const size_t down_end = L.at;
+  const size_t o_scr = L.take(W.total);
+  LGS_TRY(ctx_reserve(c, L.at, down_end));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* ioff = (uint64_t*)(h + o_ioff);
+  uint32_t* ilen = (uint32_t*)(h + o_ilen);
+  size_t ia = o_in;
+  for (uint32_t i = 0; i < n; ++i) {
+    memcpy(h + ia, raw + raw_off[i], raw_len[i]);
+    ioff[i] = ia;
+    ilen[i] = raw_len[i];
+    ia += align_up(raw_len[i], 16);
+  }
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  LGS_TRY(table_write(d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), n, max_in,
+                      compression, base, d + o_file, (uint64_t*)(d + o_hoff),
+                      (uint64_t*)(d + o_hsize), (uint64_t*)(d + o_end), d + o_scr, W, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_hoff, d + o_hoff, o_file - o_hoff, hipMemcpyDeviceToHost,
+                         c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint64_t e = *(const uint64_t*)(h + o_end);
+  const size_t bytes = (size_t)(e - base);
+  if (bytes > file_cap) return fail(LGS_EINVAL, "file buffer of %zu bytes, %zu needed", file_cap, bytes);
+  LGS_HIP(hipMemcpyAsync(h + o_file, d + o_file, bytes, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  memcpy(file, h + o_file, bytes);
+  memcpy(handle_off, h + o_hoff, 8 * (size_t)n);
+  memcpy(handle_size, h + o_hsize, 8 * (size_t)n);
+  *end = e;
+  return LGS_OK;
+}
+
+int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* handle_off,
+                        const uint64_t* handle_size, uint32_t n, int verify_checksums,
+                        uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                        uint32_t* out_len, uint8_t* status) {
+  if (n == 0) return LGS_OK;
+  if (!file || !handle_off || !handle_size || !out || !out_off || !out_cap || !out_len || !status)
+    return fail(LGS_EINVAL, "NULL argument");
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  // Only each block's byte range (+ trailer) travels, packed 16-aligned;
+  // a range outside the file keeps an out-of-range offset so the device
+  // reports the truncated read itself (format.c:195-198).
+  size_t blk_total = 0, out_total = 0;
+  uint32_t max_cap = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t o = handle_off[i], sz = handle_size[i];
+    if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE)
+      blk_total += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
+    out_total += align_up(out_cap[i], 16);
+    if (out_cap[i] > max_cap) max_cap = out_cap[i];
+  }
+  const ReadScratch R(n);
+  Layout L;
+  const size_t o_blk = L.take(blk_total + 16);
+  const size_t o_hoff = L.take(8 * (size_t)n);
+  const size_t o_hsize = L.take(8 * (size_t)n);
+  const size_t o_ooff = L.take(8 * (size_t)n);
+  const size_t o_ocap = L.take(4 * (size_t)n);
+  const size_t up_end = L.at;
+  const size_t o_st = L.take((size_t)n);
+  const size_t o_olen = L.take(4 * (size_t)n);
+  const size_t o_out = L.take(out_total + 16);
+  const size_t down_end = L.at;
+  const size_t o_scr = L.take(R.total);
+  LGS_TRY(ctx_reserve(c, L.at, down_end));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* hoff = (uint64_t*)(h + o_hoff);
+  uint64_t* hsize = (uint64_t*)(h + o_hsize);
+  uint64_t* ooff = (uint64_t*)(h + o_ooff);
+  uint32_t* ocap = (uint32_t*)(h + o_ocap);
+  size_t ba = 0, oa = o_out;
+  const uint64_t img_len = blk_total + 16;   // device file image: the packed ranges
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t o = handle_off[i], sz = handle_size[i];
+    hsize[i] = sz;
+    if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE) {
+      memcpy(h + o_blk + ba, file + o, (size_t)sz + LGS_TRAILER_SIZE);
+      hoff[i] = ba;
+      ba += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
+    } else {
+      hoff[i] = img_len + 1;
+    }
+    ooff[i] = oa;
+    ocap[i] = out_cap[i];
+    oa += align_up(out_cap[i], 16);
+  }
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  LGS_TRY(table_read(d + o_blk, img_len, (const uint64_t*)(d + o_hoff),
+                     (const uint64_t*)(d + o_hsize), n, verify_checksums, d,
+                     (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap), max_cap,
+                     (uint32_t*)(d + o_olen), d + o_st, d + o_scr, R, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint32_t* olen = (const uint32_t*)(h + o_olen);
+  for (uint32_t i = 0; i < n; ++i) {
+    status[i] = h[o_st + i];
+    out_len[i] = olen[i];
+    if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
+  }
+  return LGS_OK;
+}
+
 int lgs_device_count(void) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess) return 0;

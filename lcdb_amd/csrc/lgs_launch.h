@@ -1,8 +1,10 @@
 // lgs_launch.h -- host-side launch interface between the runtime
-// (lgs_api.cpp) and the kernels (lgs_encode.hip, lgs_decode.hip).
+// (lgs_api.cpp) and the kernels (lgs_encode.hip, lgs_decode.hip,
+// lgs_table.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace lgs {
@@ -29,5 +31,42 @@ hipError_t launch_encode_group(const EncodeArgs& a, uint32_t max_in, uint32_t la
                                hipStream_t s);
 hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                          uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s);
+
+// ---- SSTable block framing (lgs_table.hip) ----
+
+// Per-block status codes (the LGS_ST_* values of include/lcdb_gpu_snappy.h).
+constexpr uint32_t kStCorrupt = 0, kStOk = 1, kStNoSpace = 2, kStIoErr = 3, kStBadCrc = 4,
+                   kStBadType = 5;
+
+struct FrameArgs {
+  const uint8_t* raw; const uint64_t* raw_off; const uint32_t* raw_len;
+  // Encoder output; enc_len == nullptr: no compression (every block raw).
+  const uint8_t* enc; const uint64_t* enc_off; const uint32_t* enc_len;
+  uint8_t* file; uint64_t base; const uint64_t* foff;
+  uint64_t* handle_off; uint64_t* handle_size; uint32_t n;
+};
+
+struct CheckArgs {
+  const uint8_t* file; uint64_t file_len; const uint64_t* hoff; const uint64_t* hsize;
+  uint32_t verify; uint8_t* out; const uint64_t* out_off; const uint32_t* out_cap;
+  uint32_t* out_len; uint8_t* status;
+  uint64_t* dec_in_off; uint32_t* dec_len; uint64_t* dec_off; uint32_t* dec_cap;
+  uint64_t dummy_off; uint32_t n;
+};
+
+// CRC32C of each block (followed by its type byte when type != null),
+// masked (crc32c.h:46-50) or not.
+hipError_t launch_crc(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                      const uint8_t* type, int masked, uint32_t* crc, uint32_t n, hipStream_t s);
+// Exclusive scan of per-item region sizes (mode 0: 16-aligned encode bounds;
+// mode 1: framed block sizes) into u64 offsets starting at base; *end = base
+// + total when end != null.  part: scan_parts(n) u64 of device scratch.
+size_t scan_parts(uint32_t n);
+hipError_t launch_scan(int mode, const uint32_t* raw_len, const uint32_t* enc_len, uint64_t* part,
+                       uint64_t base, uint64_t* off, uint64_t* end, uint32_t n, hipStream_t s);
+hipError_t launch_frame(const FrameArgs& a, hipStream_t s);
+hipError_t launch_check(const CheckArgs& a, hipStream_t s);
+hipError_t launch_merge(uint8_t* status, uint32_t* out_len, const uint8_t* dec_status,
+                        const uint32_t* dec_out_len, uint32_t n, hipStream_t s);
 
 }  // namespace lgs

@@ -143,6 +143,100 @@ def best() -> Codec:
     return reference() or restatement()
 
 
+# -- block framing (table_oracle.c): CRC32C trailers, data-block writes,
+#    block reads; plus the reference's own crc32c.c (_ref/libref_crc32c.so) --
+
+REF_CRC_SO = os.path.join(HERE, "_ref", "libref_crc32c.so")
+ST_CORRUPT, ST_OK, ST_NOSPACE, ST_IOERR, ST_BADCRC, ST_BADTYPE = 0, 1, 2, 3, 4, 5
+
+_tab = None
+_refcrc = None
+
+
+def _table_lib():
+    global _tab
+    if _tab is None:
+        d = C.CDLL(ORACLE_SO, mode=C.RTLD_LOCAL)
+        vp, u64 = C.c_void_p, C.c_uint64
+        d.oracle_crc32c_extend.restype = C.c_uint32
+        d.oracle_crc32c_extend.argtypes = [C.c_uint32, vp, C.c_size_t]
+        d.oracle_crc32c_mask.restype = C.c_uint32
+        d.oracle_crc32c_mask.argtypes = [C.c_uint32]
+        d.oracle_crc32c_unmask.restype = C.c_uint32
+        d.oracle_crc32c_unmask.argtypes = [C.c_uint32]
+        d.oracle_table_write_blocks.restype = C.c_int
+        d.oracle_table_write_blocks.argtypes = [vp, vp, vp, C.c_uint32, C.c_int, u64, vp, vp, vp,
+                                                vp, vp]
+        d.oracle_table_read_block.restype = C.c_int
+        d.oracle_table_read_block.argtypes = [vp, u64, u64, u64, C.c_int, vp, C.c_size_t,
+                                              C.POINTER(C.c_size_t)]
+        _tab = d
+    return _tab
+
+
+def _buf(data: bytes):
+    return np.frombuffer(bytes(data) + b"\0", dtype=np.uint8)
+
+
+def crc32c(data: bytes, init: int = 0) -> int:
+    """ldb_crc32c_extend(init, data) (crc32c.c:643-750), restated."""
+    buf = _buf(data)   # keep the array alive across the call
+    return int(_table_lib().oracle_crc32c_extend(init, buf.ctypes.data, len(data)))
+
+
+def crc32c_mask(c: int) -> int:
+    return int(_table_lib().oracle_crc32c_mask(c))
+
+
+def crc32c_unmask(c: int) -> int:
+    return int(_table_lib().oracle_crc32c_unmask(c))
+
+
+def reference_crc32c() -> Optional[C.CDLL]:
+    """lcdb's own crc32c.c compiled unmodified (ldb_crc32c_extend), or None."""
+    global _refcrc
+    if _refcrc is None and os.path.exists(REF_CRC_SO):
+        d = C.CDLL(REF_CRC_SO, mode=C.RTLD_LOCAL)
+        d.ldb_crc32c_extend.restype = C.c_uint32
+        d.ldb_crc32c_extend.argtypes = [C.c_uint32, C.c_void_p, C.c_size_t]
+        _refcrc = d
+    return _refcrc
+
+
+def table_write_blocks(blocks, compression: int = 1, base: int = 0):
+    """ldb_tablegen_write_block per block (table_builder.c:123-213), restated.
+    Returns (region bytes, handle_off, handle_size, end)."""
+    n = len(blocks)
+    lens = np.array([len(b) for b in blocks], dtype=np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    raw = np.frombuffer(b"".join(blocks) + b"\0" * 16, dtype=np.uint8)
+    file = np.zeros(int(lens.sum()) + 5 * n + 16, dtype=np.uint8)
+    scratch = np.zeros(int(lens.max()) * 7 // 6 + 64 if n else 64, dtype=np.uint8)
+    hoff = np.zeros(n, dtype=np.uint64)
+    hsize = np.zeros(n, dtype=np.uint64)
+    end = np.zeros(1, dtype=np.uint64)
+    _table_lib().oracle_table_write_blocks(raw.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                           n, compression, base, file.ctypes.data,
+                                           hoff.ctypes.data, hsize.ctypes.data, end.ctypes.data,
+                                           scratch.ctypes.data)
+    e = int(end[0])
+    return file[:e - base].tobytes(), hoff, hsize, e
+
+
+def table_read_block(file, off: int, size: int, verify: bool, cap: int):
+    """ldb_read_block (format.c:162-270) on a file image, restated.
+    Returns (status, contents or None)."""
+    img = np.frombuffer(bytes(file) + b"\0" * 8, dtype=np.uint8)
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    olen = C.c_size_t(0)
+    st = _table_lib().oracle_table_read_block(img.ctypes.data, len(img) - 8, off, size,
+                                              1 if verify else 0, out.ctypes.data, cap,
+                                              C.byref(olen))
+    return st, (out[:olen.value].tobytes() if st == ST_OK else None)
+
+
 def time_cpu(codec: Codec, mode: str, buf, off, ln, threads: int, comp=None,
              min_seconds: float = 1.0, max_reps: int = 50) -> tuple[float, int]:
     """Median wall seconds of one pass over the corpus (encode or decode)."""

@@ -9,7 +9,9 @@
 #   <name>.gpu  with lcdb_amd/liblcdb_gpu_snappy.so  (the drop-in, unchanged
 #               callers: table_builder.c, format.c, t-snappy.c ...)
 # Programs: lcdb's unchanged test suites that reach the codec (test/t-*.c)
-# and our config-5 harness harness/build_table.c.  Outputs only in _ref/.
+# and our harnesses: harness/build_table.c (config 5) and harness/
+# dump_blocks.c (every block of an .ldb as ldb_read_block returns it, the
+# pin of the block-framing rows).  Outputs only in _ref/.
 #   make -C oracle -f lcdb.mk        (needs $(REF); the binaries travel)
 
 REF    ?= /root/reference
@@ -30,7 +32,7 @@ LIBSRC := $(addprefix src/util/,arena array atomic bloom buffer cache comparator
             version_set write_batch)
 TESTS  := snappy table db corruption simple recovery
 LIBOBJ := $(patsubst %,$(OUT)/obj/%.o,$(subst /,__,$(LIBSRC)))
-PROGS  := $(addprefix t-,$(TESTS)) build_table
+PROGS  := $(addprefix t-,$(TESTS)) build_table dump_blocks
 BINS   := $(foreach p,$(PROGS),$(OUT)/$(p).cpu $(OUT)/$(p).gpu)
 
 ifneq ($(wildcard $(REF)/src/util/snappy.c),)
@@ -51,6 +53,9 @@ $(OUT)/t-%.o: $(REF)/test/t-%.c
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(OUT)/build_table.o: $(HERE)harness/build_table.c
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/dump_blocks.o: $(HERE)harness/dump_blocks.c
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(OUT)/%.cpu: $(OUT)/%.o $(OUT)/refsnappy.o $(OUT)/liblcdb_core.a

@@ -1,0 +1,96 @@
+"""Test helpers for the block-framing rows (§8(f) 1-3): build .ldb files and
+read their blocks with the REFERENCE's own table code (oracle/harness,
+compiled by oracle/lcdb.mk), and parse what it returns."""
+from __future__ import annotations
+
+import os
+import struct
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "oracle", "_ref", "lcdb")
+
+LDB_OK, LDB_CORRUPTION, LDB_IOERR = 0, 30002, 30005     # include/lcdb.h:47-52
+
+# Product / oracle status -> the reference's return code (format.c:162-270).
+ST_TO_RC = {1: LDB_OK, 0: LDB_CORRUPTION, 4: LDB_CORRUPTION, 5: LDB_CORRUPTION, 3: LDB_IOERR}
+
+
+def same_outcome(st: int, rc: int) -> bool:
+    """Product/oracle status `st` vs the reference's ldb_read_block return.
+    A read outside the file is LDB_IOERR through pread ("truncated block
+    read", format.c:195-198) but the env's own errno (EINVAL) for offsets it
+    refuses outright (env_unix_impl.h:1086-1097): both are the I/O class."""
+    if st == 3:
+        return rc == LDB_IOERR or 0 < rc < 30000
+    return ST_TO_RC[st] == rc
+
+
+def binary(name: str) -> str:
+    p = os.path.join(BIN, name)
+    if not os.path.exists(p):
+        pytest.skip(f"{p} not built (make -C oracle -f lcdb.mk, needs /root/reference)")
+    return p
+
+
+def build_table(tmp, entries: int, block_size: int, kind: str = "cpu") -> str:
+    """An .ldb of db_bench fillseq entries written by lcdb's own builder."""
+    d = os.path.join(str(tmp), f"db_{kind}_{entries}_{block_size}")
+    r = subprocess.run([binary(f"build_table.{kind}"), d, str(entries), str(block_size)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "rc=0" in r.stdout, r.stdout + r.stderr
+    return os.path.join(d, "000001.ldb")
+
+
+@dataclass
+class Dump:
+    file_size: int
+    metaindex: tuple[int, int]
+    index: tuple[int, int]
+    off: np.ndarray          # uint64
+    size: np.ndarray         # uint64
+    rc: list[int]
+    contents: list[bytes]    # b"" unless rc == LDB_OK
+
+    @property
+    def n(self) -> int:
+        return len(self.rc)
+
+
+def dump_blocks(path: str, out: str, verify: bool, handles=None) -> Dump:
+    """ldb_read_block (format.c:162-270) on every block, by the reference."""
+    args = [binary("dump_blocks.cpu"), path, out, "1" if verify else "0"]
+    if handles is not None:
+        hp = out + ".handles"
+        np.asarray(handles, dtype=np.uint64).reshape(-1, 2).tofile(hp)
+        args.append(hp)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    b = open(out, "rb").read()
+    fsz, mo, ms, io_, is_ = struct.unpack_from("<5Q", b, 0)
+    (count,) = struct.unpack_from("<I", b, 40)
+    at = 44
+    off, size, rc, contents = [], [], [], []
+    for _ in range(count):
+        o, s, c, ln = struct.unpack_from("<QQiI", b, at)
+        at += 24
+        off.append(o)
+        size.append(s)
+        rc.append(c)
+        contents.append(b[at:at + ln])
+        at += ln
+    return Dump(fsz, (mo, ms), (io_, is_), np.array(off, dtype=np.uint64),
+                np.array(size, dtype=np.uint64), rc, contents)
+
+
+def corrupt(data: bytes, lo: int, hi: int, count: int, seed: int) -> bytes:
+    """Flip `count` seeded bytes of data[lo:hi)."""
+    rng = np.random.default_rng(seed)
+    b = bytearray(data)
+    for p in rng.integers(lo, hi, size=count):
+        b[int(p)] ^= int(rng.integers(1, 256))
+    return bytes(b)
