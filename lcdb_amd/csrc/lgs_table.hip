@@ -39,7 +39,6 @@ constexpr uint32_t kTrailer = 5;              // type byte + fixed32 crc (format
 constexpr uint32_t kSeg = 64;                 // bytes per lane per pass
 constexpr uint32_t kPass = kSeg * kWave;      // 4096
 constexpr uint32_t kLevels = 7;               // shifts by 64 * 2^k bytes, k = 0..6
-constexpr uint32_t kImg = kPass + 96;         // one pass staged, with alignment slack
 constexpr uint32_t kTabWords = 4 * 256 + kLevels * 128;
 
 // a * b mod P over GF(2), reflected (bit 31 is x^0).
@@ -114,25 +113,69 @@ __device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {        // crc32c.h:
   return (r >> 17) | (r << 15);
 }
 
-// Writes data indices [a, e) of an LDS image to dst + k (any alignment):
-// whole 16-byte destination granules with one 16-byte store, the ragged
-// granules at either end byte by byte.  base = LDS index of data index 0.
-__device__ __forceinline__ void copy_out(const uint8_t* img, int64_t base, gptr<uint8_t> dst,
+// One pass staged in LDS as its 1024 virtual dwords V_m (bytes 4m .. 4m+3
+// of the pass), re-aligned to the pass's byte 0 and stored at dword index
+// m + m / 16: lane L's segment (V_16L .. V_16L+15) starts at dword 17 L, so
+// the 64 lanes reading dword j of their segments hit 64 different banks.
+constexpr uint32_t kImgWords = kPass / 4 + kPass / 64 + 8;
+__device__ __forceinline__ uint32_t pidx(uint32_t m) { return m + (m >> 4); }
+
+// Stages the pass whose virtual byte 0 is data index lo: every V_m holding a
+// data byte of [a, b) (m < 1024).  Other dwords are left as they were.
+// Reads whole aligned 16-byte granules of the source (coalesced, one per
+// lane) plus the dword after each; never a granule without a byte of
+// src[a .. b + 16).
+__device__ __forceinline__ void stage_pass(uint32_t* img, gptr<const uint8_t> src, int64_t lo,
+                                           uint32_t a, uint32_t b) {
+  if (a >= b) return;
+  const uint64_t s0 = (uint64_t)(uintptr_t)src;
+  const uint64_t sb = s0 + (uint64_t)lo;                     // address of virtual byte 0
+  const uint32_t sh = (uint32_t)(sb & 3u);
+  const uint64_t ab = sb - sh;                               // V_m = bytes ab + 4m + sh ..
+  const uint64_t g_lo = (s0 + a) & ~15ull, g_hi = (s0 + b + 15) & ~15ull;
+  for (uint64_t g = g_lo + 16ull * lane_id(); g < g_hi; g += 16ull * kWave) {
+    const u32x4 q = *(gptr<const u32x4>)(src + (int64_t)(g - s0));
+    const uint32_t nx = *(gptr<const uint32_t>)(src + (int64_t)(g + 16 - s0));
+    const int32_t i0 = (int32_t)((int64_t)(g - ab) >> 2);    // dword index of q.x
+    const uint32_t v[5] = {__builtin_amdgcn_alignbyte(q.x, 0u, sh),   // bytes before g: never data
+                           __builtin_amdgcn_alignbyte(q.y, q.x, sh),
+                           __builtin_amdgcn_alignbyte(q.z, q.y, sh),
+                           __builtin_amdgcn_alignbyte(q.w, q.z, sh),
+                           __builtin_amdgcn_alignbyte(nx, q.w, sh)};
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int32_t m = i0 - 1 + r;
+      if ((r > 0 || g == g_lo) && m >= 0 && m < (int32_t)(kPass / 4)) img[pidx((uint32_t)m)] = v[r];
+    }
+  }
+}
+
+// Byte v (0 <= v < 4096 + 16) of a staged pass.
+__device__ __forceinline__ uint32_t img_byte(const uint32_t* img, uint32_t v) {
+  return (img[pidx(v >> 2)] >> (8 * (v & 3u))) & 0xffu;
+}
+
+// Writes data indices [a, e) of the staged pass (virtual byte 0 = data index
+// lo) to dst + k, any alignment: whole 16-byte destination granules with one
+// 16-byte store, the ragged granules at either end byte by byte.
+__device__ __forceinline__ void copy_out(const uint32_t* img, int64_t lo, gptr<uint8_t> dst,
                                          uint32_t a, uint32_t e) {
   if (a >= e) return;
   const uint64_t d0 = (uint64_t)(uintptr_t)dst;
   const uint64_t g_lo = (d0 + a) & ~15ull, g_hi = (d0 + e + 15) & ~15ull;
   for (uint64_t g = g_lo + 16ull * lane_id(); g < g_hi; g += 16ull * kWave) {
-    const int64_t k0 = (int64_t)(g - d0);
-    const uint32_t li = (uint32_t)(base + k0);
+    const int64_t k0 = (int64_t)(g - d0);                    // data index of the granule
     if (g >= d0 + a && g + 16 <= d0 + e) {
-      const u32x4 v{lds_ld32(img, li), lds_ld32(img, li + 4), lds_ld32(img, li + 8),
-                    lds_ld32(img, li + 12)};
+      const uint32_t v0 = (uint32_t)(k0 - lo), m0 = v0 >> 2, t = v0 & 3u;
+      const uint32_t w0 = img[pidx(m0)], w1 = img[pidx(m0 + 1)], w2 = img[pidx(m0 + 2)],
+                     w3 = img[pidx(m0 + 3)], w4 = img[pidx(m0 + 4)];
+      const u32x4 v{__builtin_amdgcn_alignbyte(w1, w0, t), __builtin_amdgcn_alignbyte(w2, w1, t),
+                    __builtin_amdgcn_alignbyte(w3, w2, t), __builtin_amdgcn_alignbyte(w4, w3, t)};
       *(gptr<u32x4>)(dst + k0) = v;
     } else {
       for (uint32_t t = 0; t < 16; ++t) {
         const int64_t k = k0 + t;
-        if (k >= (int64_t)a && k < (int64_t)e) dst[k] = img[li + t];
+        if (k >= (int64_t)a && k < (int64_t)e) dst[k] = (uint8_t)img_byte(img, (uint32_t)(k - lo));
       }
     }
   }
@@ -142,8 +185,8 @@ __device__ __forceinline__ void copy_out(const uint8_t* img, int64_t base, gptr<
 // byte `type` when has_type -- the trailer CRC of table_builder.c:139-140
 // before masking.  When `copy`, src[0 .. len) is also written to dst, and
 // the type byte after it when copy_type.  want_crc == false: copy only.
-// Uniform result.
-__device__ uint32_t wave_crc(const Crc& T, uint8_t* img, gptr<const uint8_t> src, uint32_t len,
+// Uniform result.  Reads may touch the 16 bytes after src[len - 1].
+__device__ uint32_t wave_crc(const Crc& T, uint32_t* img, gptr<const uint8_t> src, uint32_t len,
                              uint32_t has_type, uint32_t type, gptr<uint8_t> dst, bool copy,
                              bool copy_type, bool want_crc) {
   const uint32_t lane = lane_id();
@@ -164,32 +207,27 @@ __device__ uint32_t wave_crc(const Crc& T, uint8_t* img, gptr<const uint8_t> src
     const uint32_t a = lo < 0 ? 0u : (uint32_t)lo;
     const uint32_t b = (uint32_t)(lo + kPass < (int64_t)len ? lo + kPass : (int64_t)len);
     const bool last = p + 1 == passes;
-    const uint64_t sbase = (uint64_t)(uintptr_t)src + (uint64_t)lo;
-    const uint32_t c0 = 16u + (uint32_t)(sbase & 15u);        // LDS index of virtual byte 0
-    if (a < b) {                                              // stage [a, b) keeping src & 15
-      const uint64_t s0 = (uint64_t)(uintptr_t)src;
-      const uint64_t g_lo = (s0 + a) & ~15ull, g_hi = (s0 + b + 15) & ~15ull;
-      for (uint64_t g = g_lo + 16ull * lane; g < g_hi; g += 16ull * kWave) {
-        const u32x4 v = *(gptr<const u32x4>)(src + (int64_t)(g - s0));
-        *reinterpret_cast<u32x4*>(img + c0 + (uint32_t)(g - sbase)) = v;
-      }
-    }
+    stage_pass(img, src, lo, a, b);
     order();
-    if (last && has_type && lane == 0) img[c0 + (uint32_t)((int64_t)len - lo)] = (uint8_t)type;
+    if (last && has_type && lane == 0) {                      // virtual byte 4095
+      reinterpret_cast<uint8_t*>(img)[4 * pidx(kPass / 4 - 1) + 3] = (uint8_t)type;
+    }
     order();
     if (want_crc) {
       uint32_t c = 0;
+      const int64_t k0 = lo + (int64_t)(kSeg * lane);         // data index of the segment
+      if (k0 + (int64_t)kSeg > 0) {                           // lanes wholly in the padding skip
 #pragma unroll 4
-      for (uint32_t j = 0; j < kSeg / 4; ++j) {
-        const uint32_t v = kSeg * lane + 4 * j;
-        const int32_t k = (int32_t)(lo + v);                  // data index of the dword
-        const uint32_t raw = lds_ld32(img, c0 + v);
-        const uint32_t nk = (uint32_t)(-k);
-        const uint32_t part = ~0u << (8 * (nk & 3u));         // used for -4 < k < 0
-        const uint32_t vm = k >= 0 ? ~0u : (k <= -4 ? 0u : part);
-        const uint32_t head = ~0u >> (8 * ((uint32_t)k & 3u)); // used for 0 <= k < 4
-        const uint32_t cm = (k >= 4 || k <= -4) ? 0u : (k >= 0 ? head : part);
-        c = T.dword(c, (raw & vm) ^ cm);                      // ~0 pre-conditioning
+        for (uint32_t j = 0; j < kSeg / 4; ++j) {
+          const int32_t k = (int32_t)(k0 + 4 * j);            // data index of the dword
+          const uint32_t raw = img[17 * lane + j];
+          const uint32_t nk = (uint32_t)(-k);
+          const uint32_t part = ~0u << (8 * (nk & 3u));       // used for -4 < k < 0
+          const uint32_t vm = k >= 0 ? ~0u : (k <= -4 ? 0u : part);
+          const uint32_t head = ~0u >> (8 * ((uint32_t)k & 3u)); // used for 0 <= k < 4
+          const uint32_t cm = (k >= 4 || k <= -4) ? 0u : (k >= 0 ? head : part);
+          c = T.dword(c, (raw & vm) ^ cm);                    // ~0 pre-conditioning
+        }
       }
 #pragma unroll
       for (uint32_t lv = 0; lv < 6; ++lv) {                   // lanes i, i + 2^lv
@@ -199,7 +237,7 @@ __device__ uint32_t wave_crc(const Crc& T, uint8_t* img, gptr<const uint8_t> src
       const uint32_t pc = uni(c);                             // lane 0: the whole pass
       acc = p == 0 ? pc : uni(T.shift(6, vec(acc)) ^ pc);
     }
-    if (copy) copy_out(img, (int64_t)c0 - lo, dst, a, last && copy_type ? b + has_type : b);
+    if (copy) copy_out(img, lo, dst, a, last && copy_type ? b + has_type : b);
     order();
   }
   return ~acc;
@@ -213,7 +251,7 @@ __global__ __launch_bounds__(64 * WAVES) void crc_kernel(
     const uint32_t* __restrict__ in_len, const uint8_t* __restrict__ type,
     uint32_t masked, uint32_t* __restrict__ crc_out, uint32_t n) {
   __shared__ uint32_t s_tab[kTabWords];
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[WAVES][kImg];
+  __shared__ __attribute__((aligned(16))) uint32_t s_img[WAVES][kImgWords];
   load_tables(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
@@ -327,7 +365,7 @@ __global__ __launch_bounds__(64 * WAVES) void frame_kernel(
     uint8_t* __restrict__ file, uint64_t base, const uint64_t* __restrict__ foff,
     uint64_t* __restrict__ handle_off, uint64_t* __restrict__ handle_size, uint32_t n) {
   __shared__ uint32_t s_tab[kTabWords];
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[WAVES][kImg];
+  __shared__ __attribute__((aligned(16))) uint32_t s_img[WAVES][kImgWords];
   load_tables(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
@@ -368,7 +406,7 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     uint64_t* __restrict__ dec_off, uint32_t* __restrict__ dec_cap, uint64_t dummy_off,
     uint32_t n) {
   __shared__ uint32_t s_tab[kTabWords];
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[WAVES][kImg];
+  __shared__ __attribute__((aligned(16))) uint32_t s_img[WAVES][kImgWords];
   load_tables(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
@@ -434,12 +472,28 @@ __global__ __launch_bounds__(256) void merge_kernel(uint8_t* __restrict__ status
   out_len[i] = dec_out_len[i];
 }
 
-// Grid for the one-wave-per-block framing kernels: enough workgroups to
-// fill the chip, each loading the tables once and striding over blocks.
+// Grid for the one-wave-per-block framing kernels: every workgroup
+// resident at once (CUs x the occupancy the kernel's LDS allows), each
+// loading the tables once and striding over blocks -- no second, partial
+// round of workgroups.
 constexpr uint32_t kFrameWaves = 4;
-uint32_t frame_grid(uint32_t n) {
+template <class K>
+uint32_t frame_grid(K kernel, uint32_t n) {
+  static uint32_t resident = 0;   // same on every device of the node
+  if (resident == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64 * kFrameWaves, 0) !=
+            hipSuccess ||
+        cus <= 0 || per <= 0) {
+      cus = 256;
+      per = 4;
+    }
+    resident = (uint32_t)(cus * per);
+  }
   const uint32_t want = (n + kFrameWaves - 1) / kFrameWaves;
-  return want < 2048u ? (want ? want : 1u) : 2048u;
+  return want < resident ? (want ? want : 1u) : resident;
 }
 
 }  // namespace
@@ -447,8 +501,8 @@ uint32_t frame_grid(uint32_t n) {
 hipError_t launch_crc(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                       const uint8_t* type, int masked, uint32_t* crc, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc_kernel<kFrameWaves>, dim3(frame_grid(n)), dim3(64 * kFrameWaves), 0, s,
-                     in, in_off, in_len, type, (uint32_t)(masked != 0), crc, n);
+  hipLaunchKernelGGL(crc_kernel<kFrameWaves>, dim3(frame_grid(crc_kernel<kFrameWaves>, n)), dim3(64 * kFrameWaves),
+                     0, s, in, in_off, in_len, type, (uint32_t)(masked != 0), crc, n);
   return hipGetLastError();
 }
 
@@ -476,7 +530,7 @@ hipError_t launch_scan(int mode, const uint32_t* raw_len, const uint32_t* enc_le
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(frame_kernel<kFrameWaves>, dim3(frame_grid(a.n)), dim3(64 * kFrameWaves), 0,
+  hipLaunchKernelGGL(frame_kernel<kFrameWaves>, dim3(frame_grid(frame_kernel<kFrameWaves>, a.n)), dim3(64 * kFrameWaves), 0,
                      s, a.raw, a.raw_off, a.raw_len, a.enc, a.enc_off, a.enc_len, a.file, a.base,
                      a.foff, a.handle_off, a.handle_size, a.n);
   return hipGetLastError();
@@ -484,7 +538,7 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
 
 hipError_t launch_check(const CheckArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(check_kernel<kFrameWaves>, dim3(frame_grid(a.n)), dim3(64 * kFrameWaves), 0,
+  hipLaunchKernelGGL(check_kernel<kFrameWaves>, dim3(frame_grid(check_kernel<kFrameWaves>, a.n)), dim3(64 * kFrameWaves), 0,
                      s, a.file, a.file_len, a.hoff, a.hsize, a.verify, a.out, a.out_off,
                      a.out_cap, a.out_len, a.status, a.dec_in_off, a.dec_len, a.dec_off, a.dec_cap,
                      a.dummy_off, a.n);
