@@ -181,6 +181,109 @@ struct Seq {
   }
 };
 
+// The recorded ops of one chunk, emitted lane-parallel: lane k holds op k
+// (recA = copy start << 16 | copy length, recB = copy distance), each op
+// being the literal from the previous op's end (lit0 for op 0) to its copy
+// start, then the copy (snappy.c:156, :166).  Every lane sizes its op
+// (snappy.c:53-102), a wave scan places it, then
+//   1. literal bytes, 4 per trip from LDS, each lane its own op's (a trip
+//      may write up to 3 bytes past a literal: into that op's tags or the
+//      next op's first byte, both rewritten in step 3);
+//   2. literals over kLongLit bytes: all lanes on one op at a time;
+//   3. literal headers and copy tags; copies of 68+ bytes (several pieces,
+//      rare) through emit_copy, one op at a time.
+// Returns the output cursor after the k ops.
+constexpr uint32_t kLongLit = 256;
+
+// v_writelane: lane l of v = s (uniform value and lane).  The lane select
+// goes through M0: gfx950 VALU reads at most one SGPR per instruction.
+__device__ __forceinline__ void write_lane(uint32_t& v, uint32_t s, uint32_t l) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0"
+               : "+v"(v) : "s"(s), "s"(l) : "m0");
+}
+__device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, const uint8_t* x,
+                                              uint32_t recA, uint32_t recB, uint32_t k,
+                                              uint32_t lit0) {
+  const uint32_t lane = lane_id();
+  const bool live = lane < k;
+  const uint32_t base = recA >> 16, clen = recA & 0xffffu, dist = recB;
+  const uint32_t pend = (uint32_t)__shfl_up((int)(base + clen), 1);
+  const uint32_t lit = lane == 0 ? lit0 : pend;
+  const uint32_t LL = live ? base - lit : 0u;
+  const uint32_t m = LL - 1;                                          // snappy.c:55-66
+  const uint32_t hl_big = m < 256 ? 2u : 3u;
+  const uint32_t hl = LL == 0 ? 0u : (m < 60 ? 1u : hl_big);
+  const uint32_t h0_big = m < 256 ? 0xf0u : 0xf4u;
+  const uint32_t h0 = m < 60 ? (m << 2) : h0_big;
+  const uint32_t hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);
+  const bool longc = live && clen >= 68;
+  const uint32_t has60 = clen > 64 ? 3u : 0u;                         // snappy.c:84-89
+  const uint32_t rest = clen - 20 * has60;
+  const bool c1 = rest < 12 && dist < 2048;                           // snappy.c:91
+  const uint32_t first = c1 ? (((dist >> 8) << 5) | ((rest - 4) << 2) | 1u)
+                            : (((rest - 1) << 2) | 2u);
+  uint32_t ntag = has60 + (c1 ? 2u : 3u);
+  if (longc) {                                                        // snappy.c:80-89
+    const uint32_t n64 = (clen - 68) / 64 + 1;
+    uint32_t r = clen - 64 * n64;
+    const uint32_t h60 = r > 64 ? 1u : 0u;
+    r -= 60 * h60;
+    ntag = 3 * (n64 + h60) + ((r < 12 && dist < 2048) ? 2u : 3u);
+  }
+  const uint32_t size = live ? hl + LL + ntag : 0u;
+  uint32_t incl = size;
+#pragma unroll
+  for (uint32_t d = 1; d < kWave; d <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)incl, d);
+    incl += lane >= d ? t : 0u;
+  }
+  const uint32_t excl = incl - size;
+  const uint32_t total = lane_val(incl, kWave - 1);
+  const uint32_t lat = excl + hl;                                     // literal's first byte
+  const uint32_t tat = lat + LL;                                      // copy's first tag byte
+  constexpr uint32_t kOff = 0x40000000u;                              // dropped by the range check
+  // 1. short literals, lane-parallel.
+  const uint32_t LLs = LL > kLongLit ? 0u : LL;
+#pragma clang loop unroll(disable)
+  for (uint32_t t = 0; ballot(t < LLs); t += 4) {
+    const bool on = t < LLs;
+    const uint32_t v = lds_ld32(x, on ? lit + t : 0u);
+    const uint32_t vo = on ? lat + t : kOff;
+    o.put(op, vo, v);
+    o.put(op, vo + 1, v >> 8);
+    o.put(op, vo + 2, v >> 16);
+    o.put(op, vo + 3, v >> 24);
+  }
+  // 2. long literals, all lanes on one op at a time (rare).
+  for (uint64_t big = ballot(LL > kLongLit); big; big &= big - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(big);
+    const uint32_t from = lane_val(lit, l), len = lane_val(LL, l), to = lane_val(lat, l);
+#pragma clang loop unroll(disable)
+    for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
+      const uint32_t j = j0 + lane;
+      const uint32_t b = x[from + (j < len ? j : 0u)];
+      o.put(op, j < len ? to + j : kOff, b);
+    }
+  }
+  // 3. headers and tags.
+  o.put(op, hl > 0 ? excl : kOff, hdr);
+  o.put(op, hl > 1 ? excl + 1 : kOff, hdr >> 8);
+  o.put(op, hl > 2 ? excl + 2 : kOff, hdr >> 16);
+  const bool shortc = live && !longc;
+  const uint32_t fb = tat + has60;                                    // final piece
+  o.put(op, shortc && has60 ? tat : kOff, 0xeeu);
+  o.put(op, shortc && has60 ? tat + 1 : kOff, dist);
+  o.put(op, shortc && has60 ? tat + 2 : kOff, dist >> 8);
+  o.put(op, shortc ? fb : kOff, first);
+  o.put(op, shortc ? fb + 1 : kOff, dist);
+  o.put(op, shortc && !c1 ? fb + 2 : kOff, dist >> 8);
+  for (uint64_t lc = ballot(longc); lc; lc &= lc - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(lc);
+    emit_copy(o, op + lane_val(tat, l), lane_val(dist, l), lane_val(clen, l));
+  }
+  return op + total;
+}
+
 // Index of the scratch slot every table / lane-id array carries past its
 // 2048 real entries: lanes that must not touch a real entry write there
 // instead of branching around the store (keeps the batch free of exec-mask
@@ -215,6 +318,11 @@ constexpr uint32_t kSink = kTableCap;
 // A found match is extended, then its literal and copy are emitted in one
 // pass (emit_seq), then lcdb's immediate re-probe runs (snappy.c:172-186)
 // as identical work on every lane.
+//
+// DEFER: instead of emitting each literal + copy inside the next batch,
+// record the op in lane registers (v_writelane) and emit 64 ops at a time
+// lane-parallel (flush_ops): a few VALU per op instead of one 64-lane pass.
+template <bool DEFER>
 __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
                                  const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
@@ -236,6 +344,8 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
   uint32_t kv = 2;       // virtual probe index of this batch's first lane
   // The last copy's emission, deferred into the next batch (below).
   uint32_t e_lit = 0, e_L = 0, e_D = 0, e_C = 0, e_longlen = 0;
+  // DEFER: recorded ops (lane k = op k), their count, op 0's literal start.
+  uint32_t recA = 0, recB = 0, nops = 0, lit0 = 0;
 
   // Each batch takes 64 consecutive probes of a virtual sequence:
   //   v = 0: A, position at-1 -- the re-probe's first insert (snappy.c:172-175),
@@ -273,7 +383,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     // batch's LDS waits instead of lengthening the copy -> batch chain.
     // (Nothing pending: a zero-length sequence, every store dropped.)
     const Seq sq(e_lit, e_L, e_D, e_C);
-    sq.pass(o, op, x, n, 0);
+    if (!DEFER) sq.pass(o, op, x, n, 0);
 
     const bool isA = v == 0, isB = v == 1;
     const bool valid = v < 2 || (in_tab && start + o1 <= last);  // snappy.c:143
@@ -332,10 +442,12 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     order();
     tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
     order();
-    sq.rest(o, op, x, n);                                         // rare: > 64 bytes
-    op += sq.total;
-    if (e_longlen) op += emit_copy(o, op, e_D, e_longlen);        // rare: 68+ byte copy
-    e_L = e_C = e_longlen = 0;
+    if (!DEFER) {
+      sq.rest(o, op, x, n);                                       // rare: > 64 bytes
+      op += sq.total;
+      if (e_longlen) op += emit_copy(o, op, e_D, e_longlen);      // rare: 68+ byte copy
+      e_L = e_C = e_longlen = 0;
+    }
 
     bool done;
     if (mm) {
@@ -366,12 +478,22 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
       // re-match), then the copy -- emitted during the next batch (copies
       // of 68+ bytes, rare, get their tags from emit_copy).
       const uint32_t clen = at - base, dist = base - ref;
-      const bool longc = clen >= 68;
-      e_lit = lit;
-      e_L = base - lit;
-      e_D = dist;
-      e_C = longc ? 0u : clen;
-      e_longlen = longc ? clen : 0u;
+      if (DEFER) {
+        write_lane(recA, (base << 16) | clen, nops);
+        write_lane(recB, dist, nops);
+        if (++nops == kWave) {                                    // every 64 ops
+          op = flush_ops(o, op, x, recA, recB, kWave, lit0);
+          nops = 0;
+          lit0 = at;
+        }
+      } else {
+        const bool longc = clen >= 68;
+        e_lit = lit;
+        e_L = base - lit;
+        e_D = dist;
+        e_C = longc ? 0u : clen;
+        e_longlen = longc ? clen : 0u;
+      }
       lit = at;
       done = at >= last;                                          // snappy.c:169
       start = at + 1;                                             // snappy.c:184-185
@@ -384,7 +506,9 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     }
     if (done) break;
   }
-  {                                                               // the last copy's emission
+  if (DEFER) {
+    if (nops) op = flush_ops(o, op, x, recA, recB, nops, lit0);
+  } else {                                                        // the last copy's emission
     const Seq sq(e_lit, e_L, e_D, e_C);
     sq.pass(o, op, x, n, 0);
     sq.rest(o, op, x, n);
@@ -399,7 +523,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
 // Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
 // its varint32 length (snappy.c:368).  Otherwise hdr[i] is the varint value
 // to prefix, or 0xffffffff for none (a later chunk of a > 64 KiB block).
-template <uint32_t IN_CAP, uint32_t WAVES>
+template <uint32_t IN_CAP, uint32_t WAVES, bool DEFER>
 __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -451,7 +575,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* x = &s_in[wv][sh];
     order();
     if (clen >= kMinBlock) {
-      op = encode_chunk(x, clen, &s_tab[wv][0], o, op, off0, off1);
+      op = encode_chunk<DEFER>(x, clen, &s_tab[wv][0], o, op, off0, off1);
     } else {
       op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
@@ -477,8 +601,15 @@ __global__ __launch_bounds__(256) void concat_kernel(
 template <uint32_t IN_CAP, uint32_t WAVES>
 static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
   const uint32_t grid = (a.n + WAVES - 1) / WAVES;
-  hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
-                     a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n);
+  // LGS_ENCODE_EMIT=inline: the per-batch emission variant (A/B).
+  const char* emit = getenv("LGS_ENCODE_EMIT");
+  if (emit && !strcmp(emit, "inline")) {
+    hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES, false>), dim3(grid), dim3(64 * WAVES), 0, s,
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n);
+  } else {
+    hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES, true>), dim3(grid), dim3(64 * WAVES), 0, s,
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n);
+  }
   return hipGetLastError();
 }
 
