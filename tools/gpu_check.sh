@@ -27,7 +27,7 @@ for s in $steps; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-             --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-parity ;;
+             --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pipelined ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
