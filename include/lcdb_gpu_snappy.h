@@ -177,6 +177,35 @@ int lgs_table_read_host(const uint8_t *file, uint64_t file_len,
                         const uint64_t *out_off, const uint32_t *out_cap,
                         uint32_t *out_len, uint8_t *status);
 
+/* Row 4.  lcdb's builtin bloom filter (src/util/bloom.c, src/util/hash.c):
+   filter f holds keys [first[f], first[f+1]) and is written at out +
+   out_off[f] exactly as ldb_bloom_build appends it (bloom.c:102-119):
+   lgs_bloom_filter_size(n, bits_per_key) bytes = the bit array
+   (max(64, n * bits_per_key) bits, rounded up to bytes) + one byte k
+   (bits_per_key * 0.69, clamped to [1, 30]); an empty filter has no bytes
+   (filter_block.c:89-93).  match[q] = ldb_bloom_match(filter
+   query_filter[q], key q) (bloom.c:121-165).  Keys must stay readable 16
+   bytes past their end.  The _dev calls are asynchronous. */
+size_t lgs_bloom_filter_size(uint32_t nkeys, int bits_per_key);
+int lgs_bloom_build_dev(const uint8_t *d_keys, const uint64_t *d_key_off,
+                        const uint32_t *d_key_len, const uint32_t *d_first,
+                        uint32_t nfilters, int bits_per_key, uint8_t *d_out,
+                        const uint64_t *d_out_off, void *stream);
+int lgs_bloom_match_dev(const uint8_t *d_filters, const uint64_t *d_filter_off,
+                        const uint32_t *d_filter_len, const uint32_t *d_query_filter,
+                        const uint8_t *d_keys, const uint64_t *d_key_off,
+                        const uint32_t *d_key_len, uint8_t *d_match, uint32_t nq,
+                        void *stream);
+int lgs_bloom_build_host(const uint8_t *keys, const uint64_t *key_off,
+                         const uint32_t *key_len, const uint32_t *first,
+                         uint32_t nfilters, int bits_per_key, uint8_t *out,
+                         const uint64_t *out_off);
+int lgs_bloom_match_host(const uint8_t *filters, const uint64_t *filter_off,
+                         const uint32_t *filter_len, uint32_t nfilters,
+                         const uint32_t *query_filter, const uint8_t *keys,
+                         const uint64_t *key_off, const uint32_t *key_len, uint32_t nq,
+                         uint8_t *match);
+
 /* Devices and diagnostics. */
 int lgs_device_count(void);
 int lgs_set_device(int device);  /* device used by the calling thread */

@@ -725,6 +725,183 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
   return LGS_OK;
 }
 
+// ---- bloom filter (kernels: lgs_bloom.hip) ----
+
+namespace {
+
+uint32_t bloom_k(int bpk) {                        // bloom.c:35-45
+  size_t k = (size_t)(bpk * 0.69);
+  if (k < 1) k = 1;
+  if (k > 30) k = 30;
+  return (uint32_t)k;
+}
+
+size_t bloom_bytes(uint64_t n, int bpk) {          // bloom.c:69-80
+  uint64_t bits = n * (uint64_t)bpk;
+  if (bits < 64) bits = 64;
+  return (size_t)((bits + 7) / 8);
+}
+
+constexpr int kMaxBitsPerKey = 1 << 16;
+
+}  // namespace
+
+size_t lgs_bloom_filter_size(uint32_t nkeys, int bits_per_key) {
+  if (nkeys == 0 || bits_per_key < 0) return 0;
+  return bloom_bytes(nkeys, bits_per_key) + 1;
+}
+
+int lgs_bloom_build_dev(const uint8_t* d_keys, const uint64_t* d_key_off,
+                        const uint32_t* d_key_len, const uint32_t* d_first, uint32_t nfilters,
+                        int bits_per_key, uint8_t* d_out, const uint64_t* d_out_off,
+                        void* stream) {
+  if (nfilters == 0) return LGS_OK;
+  if (!d_keys || !d_key_off || !d_key_len || !d_first || !d_out || !d_out_off)
+    return fail(LGS_EINVAL, "NULL argument");
+  if (bits_per_key < 0 || bits_per_key > kMaxBitsPerKey)
+    return fail(LGS_EINVAL, "bits_per_key %d out of range", bits_per_key);
+  LGS_HIP(launch_bloom_build(d_keys, d_key_off, d_key_len, d_first, nfilters,
+                             (uint32_t)bits_per_key, bloom_k(bits_per_key), d_out, d_out_off,
+                             (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_bloom_match_dev(const uint8_t* d_filters, const uint64_t* d_filter_off,
+                        const uint32_t* d_filter_len, const uint32_t* d_query_filter,
+                        const uint8_t* d_keys, const uint64_t* d_key_off,
+                        const uint32_t* d_key_len, uint8_t* d_match, uint32_t nq, void* stream) {
+  if (nq == 0) return LGS_OK;
+  if (!d_filters || !d_filter_off || !d_filter_len || !d_query_filter || !d_keys || !d_key_off ||
+      !d_key_len || !d_match)
+    return fail(LGS_EINVAL, "NULL argument");
+  LGS_HIP(launch_bloom_match(d_filters, d_filter_off, d_filter_len, d_query_filter, d_keys,
+                             d_key_off, d_key_len, d_match, nq, (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_bloom_build_host(const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len,
+                         const uint32_t* first, uint32_t nfilters, int bits_per_key,
+                         uint8_t* out, const uint64_t* out_off) {
+  if (nfilters == 0) return LGS_OK;
+  if (!keys || !key_off || !key_len || !first || !out || !out_off)
+    return fail(LGS_EINVAL, "NULL argument");
+  if (bits_per_key < 0 || bits_per_key > kMaxBitsPerKey)
+    return fail(LGS_EINVAL, "bits_per_key %d out of range", bits_per_key);
+  for (uint32_t f = 0; f < nfilters; ++f)
+    if (first[f + 1] < first[f]) return fail(LGS_EINVAL, "first[] decreases at filter %u", f);
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  const uint32_t nkeys = first[nfilters] - first[0];
+  const uint32_t k0 = first[0];
+  size_t key_bytes = 0, filt_bytes = 0;
+  for (uint32_t i = k0; i < k0 + nkeys; ++i) key_bytes += key_len[i];
+  for (uint32_t f = 0; f < nfilters; ++f)
+    filt_bytes += lgs_bloom_filter_size(first[f + 1] - first[f], bits_per_key);
+  Layout L;  // upload | download
+  const size_t o_keys = L.take(key_bytes + 16);
+  const size_t o_koff = L.take(8 * (size_t)nkeys);
+  const size_t o_klen = L.take(4 * (size_t)nkeys);
+  const size_t o_first = L.take(4 * ((size_t)nfilters + 1));
+  const size_t o_foff = L.take(8 * (size_t)nfilters);
+  const size_t up_end = L.at;
+  const size_t o_filt = L.take(filt_bytes + 16);
+  const size_t down_end = L.at;
+  LGS_TRY(ctx_reserve(c, down_end, down_end));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* koff = (uint64_t*)(h + o_koff);
+  uint32_t* klen = (uint32_t*)(h + o_klen);
+  uint32_t* fst = (uint32_t*)(h + o_first);
+  uint64_t* foff = (uint64_t*)(h + o_foff);
+  size_t at = o_keys;
+  for (uint32_t j = 0; j < nkeys; ++j) {
+    memcpy(h + at, keys + key_off[k0 + j], key_len[k0 + j]);
+    koff[j] = at;
+    klen[j] = key_len[k0 + j];
+    at += key_len[k0 + j];
+  }
+  memset(h + at, 0, 16);
+  size_t fat = 0;
+  for (uint32_t f = 0; f <= nfilters; ++f) fst[f] = first[f] - k0;
+  for (uint32_t f = 0; f < nfilters; ++f) {
+    foff[f] = fat;
+    fat += lgs_bloom_filter_size(first[f + 1] - first[f], bits_per_key);
+  }
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  LGS_HIP(launch_bloom_build(d, (const uint64_t*)(d + o_koff), (const uint32_t*)(d + o_klen),
+                             (const uint32_t*)(d + o_first), nfilters, (uint32_t)bits_per_key,
+                             bloom_k(bits_per_key), d + o_filt, (const uint64_t*)(d + o_foff),
+                             c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_filt, d + o_filt, filt_bytes, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  for (uint32_t f = 0; f < nfilters; ++f)
+    memcpy(out + out_off[f], h + o_filt + foff[f],
+           lgs_bloom_filter_size(first[f + 1] - first[f], bits_per_key));
+  return LGS_OK;
+}
+
+int lgs_bloom_match_host(const uint8_t* filters, const uint64_t* filter_off,
+                         const uint32_t* filter_len, uint32_t nfilters,
+                         const uint32_t* query_filter, const uint8_t* keys,
+                         const uint64_t* key_off, const uint32_t* key_len, uint32_t nq,
+                         uint8_t* match) {
+  if (nq == 0) return LGS_OK;
+  if (!filters || !filter_off || !filter_len || !query_filter || !keys || !key_off || !key_len ||
+      !match)
+    return fail(LGS_EINVAL, "NULL argument");
+  for (uint32_t q = 0; q < nq; ++q)
+    if (query_filter[q] >= nfilters)
+      return fail(LGS_EINVAL, "query %u names filter %u of %u", q, query_filter[q], nfilters);
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  size_t fb = 0, kb = 0;
+  for (uint32_t f = 0; f < nfilters; ++f) fb += filter_len[f];
+  for (uint32_t q = 0; q < nq; ++q) kb += key_len[q];
+  Layout L;
+  const size_t o_f = L.take(fb + 16);
+  const size_t o_foff = L.take(8 * (size_t)nfilters);
+  const size_t o_flen = L.take(4 * (size_t)nfilters);
+  const size_t o_qf = L.take(4 * (size_t)nq);
+  const size_t o_k = L.take(kb + 16);
+  const size_t o_koff = L.take(8 * (size_t)nq);
+  const size_t o_klen = L.take(4 * (size_t)nq);
+  const size_t up_end = L.at;
+  const size_t o_m = L.take(nq);
+  const size_t down_end = L.at;
+  LGS_TRY(ctx_reserve(c, down_end, down_end));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* foff = (uint64_t*)(h + o_foff);
+  uint32_t* flen = (uint32_t*)(h + o_flen);
+  uint64_t* koff = (uint64_t*)(h + o_koff);
+  uint32_t* klen = (uint32_t*)(h + o_klen);
+  size_t at = 0;
+  for (uint32_t f = 0; f < nfilters; ++f) {
+    memcpy(h + o_f + at, filters + filter_off[f], filter_len[f]);
+    foff[f] = at;
+    flen[f] = filter_len[f];
+    at += filter_len[f];
+  }
+  memset(h + o_f + at, 0, 16);
+  memcpy(h + o_qf, query_filter, 4 * (size_t)nq);
+  at = 0;
+  for (uint32_t q = 0; q < nq; ++q) {
+    memcpy(h + o_k + at, keys + key_off[q], key_len[q]);
+    koff[q] = at;
+    klen[q] = key_len[q];
+    at += key_len[q];
+  }
+  memset(h + o_k + at, 0, 16);
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  LGS_HIP(launch_bloom_match(d + o_f, (const uint64_t*)(d + o_foff), (const uint32_t*)(d + o_flen),
+                             (const uint32_t*)(d + o_qf), d + o_k, (const uint64_t*)(d + o_koff),
+                             (const uint32_t*)(d + o_klen), d + o_m, nq, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_m, d + o_m, nq, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  memcpy(match, h + o_m, nq);
+  return LGS_OK;
+}
+
 int lgs_device_count(void) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess) return 0;

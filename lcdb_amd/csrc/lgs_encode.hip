@@ -195,11 +195,17 @@ struct Seq {
 // Returns the output cursor after the k ops.
 constexpr uint32_t kLongLit = 256;
 
-// v_writelane: lane l of v = s (uniform value and lane).  The lane select
-// goes through M0: gfx950 VALU reads at most one SGPR per instruction.
-__device__ __forceinline__ void write_lane(uint32_t& v, uint32_t s, uint32_t l) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0"
-               : "+v"(v) : "s"(s), "s"(l) : "m0");
+// v_writelane: lane l of a = sa and of b = sb (uniform values and lane).
+// The lane select goes through M0 (gfx950 VALU reads at most one SGPR per
+// instruction); M0 is compiler-reserved, so it is saved and restored inside
+// the statement.
+__device__ __forceinline__ void write_lane2(uint32_t& a, uint32_t sa, uint32_t& b, uint32_t sb,
+                                            uint32_t l) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %2, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
+      "v_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0\n\ts_mov_b32 m0, %2"
+      : "+v"(a), "+v"(b), "=&s"(keep) : "s"(sa), "s"(sb), "s"(l));
 }
 __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, const uint8_t* x,
                                               uint32_t recA, uint32_t recB, uint32_t k,
@@ -479,8 +485,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
       // of 68+ bytes, rare, get their tags from emit_copy).
       const uint32_t clen = at - base, dist = base - ref;
       if (DEFER) {
-        write_lane(recA, (base << 16) | clen, nops);
-        write_lane(recB, dist, nops);
+        write_lane2(recA, (base << 16) | clen, recB, dist, nops);
         if (++nops == kWave) {                                    // every 64 ops
           op = flush_ops(o, op, x, recA, recB, kWave, lit0);
           nops = 0;

@@ -69,4 +69,19 @@ hipError_t launch_check(const CheckArgs& a, hipStream_t s);
 hipError_t launch_merge(uint8_t* status, uint32_t* out_len, const uint8_t* dec_status,
                         const uint32_t* dec_out_len, uint32_t n, hipStream_t s);
 
+// ---- bloom filter (lgs_bloom.hip) ----
+
+// Filters f = keys [first[f], first[f+1]) written at out + out_off[f]
+// (bloom.c:102-119); bpk = bits per key, k = probes (bloom.c:35-45).
+hipError_t launch_bloom_build(const uint8_t* keys, const uint64_t* key_off,
+                              const uint32_t* key_len, const uint32_t* first, uint32_t nfilters,
+                              uint32_t bpk, uint32_t k, uint8_t* out, const uint64_t* out_off,
+                              hipStream_t s);
+// match[q] = bloom_match(filter qfilter[q], key q) (bloom.c:121-165).
+hipError_t launch_bloom_match(const uint8_t* filters, const uint64_t* filter_off,
+                              const uint32_t* filter_len, const uint32_t* qfilter,
+                              const uint8_t* keys, const uint64_t* key_off,
+                              const uint32_t* key_len, uint8_t* match, uint32_t nq,
+                              hipStream_t s);
+
 }  // namespace lgs

@@ -237,6 +237,71 @@ def table_read_block(file, off: int, size: int, verify: bool, cap: int):
     return st, (out[:olen.value].tobytes() if st == ST_OK else None)
 
 
+# -- bloom filter (bloom_oracle.c) and the reference's own bloom.c + hash.c
+#    behind oracle/harness/bloom_ref.c (_ref/lcdb/libref_bloom.so) --
+
+REF_BLOOM_SO = os.path.join(HERE, "_ref", "lcdb", "libref_bloom.so")
+
+
+class Bloom:
+    """ldb_hash / ldb_bloom_build / ldb_bloom_match behind one interface."""
+
+    def __init__(self, path: str, hash_fn: str, build_fn: str, match_fn: str, name: str,
+                 with_cap: bool):
+        d = C.CDLL(path, mode=C.RTLD_LOCAL)
+        vp, sz = C.c_void_p, C.c_size_t
+        self.name, self.with_cap = name, with_cap
+        self.f_hash = getattr(d, hash_fn)
+        self.f_hash.restype, self.f_hash.argtypes = C.c_uint32, [vp, sz, C.c_uint32]
+        self.f_build = getattr(d, build_fn)
+        self.f_build.restype = sz
+        self.f_build.argtypes = [vp, vp, vp, sz, C.c_int, vp] + ([sz] if with_cap else [])
+        self.f_match = getattr(d, match_fn)
+        self.f_match.restype, self.f_match.argtypes = C.c_int, [vp, sz, vp, sz]
+
+    def hash(self, data: bytes, seed: int) -> int:
+        b = _buf(data)
+        return int(self.f_hash(b.ctypes.data, len(data), seed))
+
+    def build(self, keys, bits_per_key: int = 10) -> bytes:
+        lens = np.array([len(k) for k in keys], dtype=np.uint32)
+        offs = np.zeros(len(keys), dtype=np.uint64)
+        if len(keys):
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        base = np.frombuffer(b"".join(keys) + b"\0" * 8, dtype=np.uint8)
+        cap = max(64, len(keys) * max(bits_per_key, 0)) // 8 + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        args = [base.ctypes.data, offs.ctypes.data, lens.ctypes.data, len(keys), bits_per_key,
+                out.ctypes.data] + ([cap] if self.with_cap else [])
+        n = self.f_build(*args)
+        return out[:n].tobytes()
+
+    def match(self, filt: bytes, key: bytes) -> bool:
+        f, k = _buf(filt), _buf(key)
+        return bool(self.f_match(f.ctypes.data, len(filt), k.ctypes.data, len(key)))
+
+
+_bloom_orc = None
+_bloom_ref = None
+
+
+def bloom_restatement() -> Bloom:
+    global _bloom_orc
+    if _bloom_orc is None:
+        _bloom_orc = Bloom(ORACLE_SO, "oracle_hash", "oracle_bloom_build", "oracle_bloom_match",
+                           "oracle", False)
+    return _bloom_orc
+
+
+def bloom_reference() -> Optional[Bloom]:
+    """lcdb's own bloom.c + hash.c (oracle/lcdb.mk), or None if not built."""
+    global _bloom_ref
+    if _bloom_ref is None and os.path.exists(REF_BLOOM_SO):
+        _bloom_ref = Bloom(REF_BLOOM_SO, "ref_hash", "ref_bloom_build", "ref_bloom_match",
+                           "reference", True)
+    return _bloom_ref
+
+
 def time_cpu(codec: Codec, mode: str, buf, off, ln, threads: int, comp=None,
              min_seconds: float = 1.0, max_reps: int = 50) -> tuple[float, int]:
     """Median wall seconds of one pass over the corpus (encode or decode)."""

@@ -36,7 +36,7 @@ PROGS  := $(addprefix t-,$(TESTS)) build_table dump_blocks
 BINS   := $(foreach p,$(PROGS),$(OUT)/$(p).cpu $(OUT)/$(p).gpu)
 
 ifneq ($(wildcard $(REF)/src/util/snappy.c),)
-all: $(BINS)
+all: $(BINS) $(OUT)/libref_bloom.so
 
 $(OUT)/obj/%.o:
 	@mkdir -p $(OUT)/obj
@@ -57,6 +57,10 @@ $(OUT)/build_table.o: $(HERE)harness/build_table.c
 
 $(OUT)/dump_blocks.o: $(HERE)harness/dump_blocks.c
 	$(CC) $(CFLAGS) -c $< -o $@
+
+# The reference's bloom filter behind a ctypes-callable shim (bloom row pin).
+$(OUT)/libref_bloom.so: $(HERE)harness/bloom_ref.c $(OUT)/liblcdb_core.a
+	$(CC) $(CFLAGS) -shared $< $(OUT)/liblcdb_core.a -lpthread -o $@
 
 $(OUT)/%.cpu: $(OUT)/%.o $(OUT)/refsnappy.o $(OUT)/liblcdb_core.a
 	$(CC) $^ -lpthread -o $@
