@@ -59,6 +59,8 @@ int ldb_snappy_decode(uint8_t *zp, const uint8_t *xp, size_t xn);
 #define LGS_EHIP       -2   /* HIP runtime error                        */
 #define LGS_ENODEV     -3   /* no usable gfx950 device                  */
 #define LGS_ENOMEM     -4   /* device / pinned allocation failed        */
+#define LGS_ENOSPC     -5   /* output buffer too small                  */
+#define LGS_EINTERNAL  -6   /* a device result broke its own bound      */
 
 /* Per-block decode status written by the decode calls. */
 #define LGS_ST_CORRUPT  0   /* reference decode would return 0          */
@@ -205,6 +207,52 @@ int lgs_bloom_match_host(const uint8_t *filters, const uint64_t *filter_off,
                          const uint32_t *query_filter, const uint8_t *keys,
                          const uint64_t *key_off, const uint32_t *key_len, uint32_t nq,
                          uint8_t *match);
+
+/* Row 4, the filter block of one table (src/table/filter_block.c), as
+   lcdb's table builder makes it: data block b holds keys [block_first[b],
+   block_first[b+1]) and sits at file offset block_off[b] (file order, the
+   first at 0); data_end is the offset after the last one.  The builder adds
+   each block's keys, writes the block, then calls
+   ldb_filtergen_start_block(offset after it) (table_builder.c:242-243,
+   276-277) and ldb_filtergen_finish at the end (:294): one bloom filter per
+   started 2 KiB of data offsets (filter_block.c:79-121), then the u32
+   offset array, its start and base_lg = 11 (:131-150).  internal_keys = 1
+   is the DB's internal filter policy (dbformat.c:308-334): keys are internal
+   keys and filters cover the user key, i.e. all but the last 8 bytes.
+   Keys must stay readable 16 bytes past their end; block_first and
+   block_off must not decrease, block_off[nblocks-1] <= data_end (checked by
+   _host; the _dev caller's contract, as for handles from lgs_table_write_dev).
+   Sizes: lgs_filter_block_bound(...) bytes of out suffice;
+   lgs_filter_block_scratch(data_end) bytes of device scratch for _dev, whose
+   block length lands in *d_size.  The _dev calls are asynchronous. */
+size_t lgs_filter_block_bound(uint32_t nkeys, uint32_t nblocks, uint64_t data_end,
+                              int bits_per_key);
+size_t lgs_filter_block_scratch(uint64_t data_end);
+int lgs_filter_block_build_dev(const uint8_t *d_keys, const uint64_t *d_key_off,
+                               const uint32_t *d_key_len, uint32_t nkeys,
+                               const uint32_t *d_block_first, const uint64_t *d_block_off,
+                               uint32_t nblocks, uint64_t data_end, int bits_per_key,
+                               int internal_keys, uint8_t *d_out, size_t out_cap,
+                               uint64_t *d_size, void *d_scratch, size_t scratch_bytes,
+                               void *stream);
+int lgs_filter_block_build_host(const uint8_t *keys, const uint64_t *key_off,
+                                const uint32_t *key_len, const uint32_t *block_first,
+                                const uint64_t *block_off, uint32_t nblocks, uint64_t data_end,
+                                int bits_per_key, int internal_keys, uint8_t *out,
+                                size_t out_cap, size_t *size);
+/* ldb_filter_matches (filter_block.c:170-225) of the filter block
+   block[0 .. block_len) -- as ldb_filter_init parses it -- for query q =
+   (key q, the data block at file offset block_offset[q]): 0 = the key is
+   certainly absent from that block, 1 = it may be present (also for every
+   malformed filter block or offset out of its range). */
+int lgs_filter_block_match_dev(const uint8_t *d_block, size_t block_len,
+                               const uint64_t *d_block_offset, const uint8_t *d_keys,
+                               const uint64_t *d_key_off, const uint32_t *d_key_len, uint32_t nq,
+                               int internal_keys, uint8_t *d_match, void *stream);
+int lgs_filter_block_match_host(const uint8_t *block, size_t block_len,
+                                const uint64_t *block_offset, const uint8_t *keys,
+                                const uint64_t *key_off, const uint32_t *key_len, uint32_t nq,
+                                int internal_keys, uint8_t *match);
 
 /* Devices and diagnostics. */
 int lgs_device_count(void);

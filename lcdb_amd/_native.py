@@ -11,6 +11,7 @@ import os
 from .build import LIB
 
 LGS_OK = 0
+LGS_EINVAL, LGS_EHIP, LGS_ENODEV, LGS_ENOMEM, LGS_ENOSPC, LGS_EINTERNAL = -1, -2, -3, -4, -5, -6
 LGS_ST_CORRUPT, LGS_ST_OK, LGS_ST_NOSPACE = 0, 1, 2
 LGS_ST_IOERR, LGS_ST_BADCRC, LGS_ST_BADTYPE = 3, 4, 5
 LGS_NO_COMPRESSION, LGS_SNAPPY_COMPRESSION = 0, 1
@@ -47,6 +48,18 @@ _SIGS = {
     "lgs_bloom_build_host": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_int, _vp, _vp]),
     "lgs_bloom_match_host": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, _vp, _vp,
                                        C.c_uint32, _vp]),
+    "lgs_filter_block_bound": (C.c_size_t, [C.c_uint32, C.c_uint32, C.c_uint64, C.c_int]),
+    "lgs_filter_block_scratch": (C.c_size_t, [C.c_uint64]),
+    "lgs_filter_block_build_dev": (C.c_int, [_vp, _vp, _vp, C.c_uint32, _vp, _vp, C.c_uint32,
+                                             C.c_uint64, C.c_int, C.c_int, _vp, C.c_size_t, _vp,
+                                             _vp, C.c_size_t, _vp]),
+    "lgs_filter_block_build_host": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_uint32, C.c_uint64,
+                                              C.c_int, C.c_int, _vp, C.c_size_t,
+                                              C.POINTER(C.c_size_t)]),
+    "lgs_filter_block_match_dev": (C.c_int, [_vp, C.c_size_t, _vp, _vp, _vp, _vp, C.c_uint32,
+                                             C.c_int, _vp, _vp]),
+    "lgs_filter_block_match_host": (C.c_int, [_vp, C.c_size_t, _vp, _vp, _vp, _vp, C.c_uint32,
+                                              C.c_int, _vp]),
     "lgs_device_count": (C.c_int, []),
     "lgs_set_device": (C.c_int, [C.c_int]),
     "lgs_last_error": (C.c_char_p, []),

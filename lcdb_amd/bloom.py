@@ -6,7 +6,12 @@ Python face of the batched C ABI (``include/lcdb_gpu_snappy.h``):
   for byte what ``ldb_bloom_build`` appends (src/util/bloom.c:102-119);
 * ``match_host(filters, queries)``: ``ldb_bloom_match`` per (filter, key)
   (bloom.c:121-165);
-* ``build`` / ``match`` on device tensors (int64 offsets, int32 lengths).
+* ``build`` / ``match`` on device tensors (int64 offsets, int32 lengths);
+* ``filter_block_host(blocks, block_off, data_end)``: a table's filter block
+  as lcdb's table builder writes it (src/table/filter_block.c:79-150), and
+  ``filter_block_match_host(block, queries)``: ``ldb_filter_matches``
+  (filter_block.c:170-225); ``filter_block_build`` / ``filter_block_match``
+  on device tensors.
 
 Everything runs through ``liblcdb_gpu_snappy.so``; there is no CPU fallback.
 """
@@ -22,7 +27,9 @@ from .snappy import _stream_ptr
 
 _L = _native.lib()
 
-__all__ = ["filter_size", "build_host", "match_host", "build", "match"]
+__all__ = ["filter_size", "build_host", "match_host", "build", "match", "filter_block_bound",
+           "filter_block_scratch", "filter_block_host", "filter_block_match_host",
+           "filter_block_build", "filter_block_match"]
 
 
 def filter_size(nkeys: int, bits_per_key: int = 10) -> int:
@@ -89,3 +96,74 @@ def match(d_filters, d_filter_off, d_filter_len, d_query_filter, d_keys, d_key_o
                                  d_keys.data_ptr(), d_key_off.data_ptr(), d_key_len.data_ptr(),
                                  d_match.data_ptr(), n, _stream_ptr(stream)),
           "lgs_bloom_match_dev")
+
+
+# ---- the filter block of one table (filter_block.c) ----
+
+def filter_block_bound(nkeys: int, nblocks: int, data_end: int, bits_per_key: int = 10) -> int:
+    return int(_L.lgs_filter_block_bound(nkeys, nblocks, data_end, bits_per_key))
+
+
+def filter_block_scratch(data_end: int) -> int:
+    return int(_L.lgs_filter_block_scratch(data_end))
+
+
+def filter_block_host(blocks: Sequence[Sequence[bytes]], block_off: Sequence[int], data_end: int,
+                      bits_per_key: int = 10, internal_keys: bool = False) -> bytes:
+    """blocks[b] = the keys of data block b in file order, block_off[b] its
+    file offset, data_end the offset after the last data block."""
+    import ctypes as C
+    keys = [k for g in blocks for k in g]
+    buf, offs, lens = _pack(keys)
+    first = np.zeros(len(blocks) + 1, dtype=np.uint32)
+    first[1:] = np.cumsum([len(g) for g in blocks], dtype=np.uint64)
+    boff = np.array(list(block_off) + [0], dtype=np.uint64)
+    cap = filter_block_bound(len(keys), len(blocks), data_end, bits_per_key)
+    out = np.zeros(cap + 1, dtype=np.uint8)
+    size = C.c_size_t(0)
+    check(_L.lgs_filter_block_build_host(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                         first.ctypes.data, boff.ctypes.data, len(blocks),
+                                         data_end, bits_per_key, int(internal_keys),
+                                         out.ctypes.data, cap, C.byref(size)),
+          "lgs_filter_block_build_host")
+    return out[:size.value].tobytes()
+
+
+def filter_block_match_host(block: bytes, queries: Sequence[tuple[int, bytes]],
+                            internal_keys: bool = False) -> np.ndarray:
+    """uint8 array: ldb_filter_matches(block, data block offset, key) per query."""
+    bb = np.frombuffer(bytes(block) + b"\0" * 16, dtype=np.uint8)
+    kbuf, koff, klen = _pack([k for _, k in queries])
+    qo = np.array([o for o, _ in queries] + [0], dtype=np.uint64)
+    m = np.zeros(len(queries), dtype=np.uint8)
+    check(_L.lgs_filter_block_match_host(bb.ctypes.data, len(block), qo.ctypes.data,
+                                         kbuf.ctypes.data, koff.ctypes.data, klen.ctypes.data,
+                                         len(queries), int(internal_keys), m.ctypes.data),
+          "lgs_filter_block_match_host")
+    return m
+
+
+def filter_block_build(d_keys, d_key_off, d_key_len, d_block_first, d_block_off, data_end,
+                       bits_per_key, d_out, d_size, d_scratch, internal_keys=False, stream=None):
+    """Asynchronously build the filter block of int(d_block_first.numel()) - 1
+    data blocks into d_out (length -> d_size[0])."""
+    nb = int(d_block_first.numel()) - 1
+    check(_L.lgs_filter_block_build_dev(d_keys.data_ptr(), d_key_off.data_ptr(),
+                                        d_key_len.data_ptr(), int(d_key_len.numel()),
+                                        d_block_first.data_ptr(), d_block_off.data_ptr(), nb,
+                                        data_end, bits_per_key, int(internal_keys),
+                                        d_out.data_ptr(), d_out.numel(), d_size.data_ptr(),
+                                        d_scratch.data_ptr(), d_scratch.numel(),
+                                        _stream_ptr(stream)),
+          "lgs_filter_block_build_dev")
+
+
+def filter_block_match(d_block, block_len, d_block_offset, d_keys, d_key_off, d_key_len, d_match,
+                       internal_keys=False, stream=None):
+    """Asynchronously answer int(d_block_offset.numel()) filter-block queries."""
+    n = int(d_block_offset.numel())
+    check(_L.lgs_filter_block_match_dev(d_block.data_ptr(), block_len, d_block_offset.data_ptr(),
+                                        d_keys.data_ptr(), d_key_off.data_ptr(),
+                                        d_key_len.data_ptr(), n, int(internal_keys),
+                                        d_match.data_ptr(), _stream_ptr(stream)),
+          "lgs_filter_block_match_dev")

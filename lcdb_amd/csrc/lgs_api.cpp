@@ -762,7 +762,7 @@ int lgs_bloom_build_dev(const uint8_t* d_keys, const uint64_t* d_key_off,
     return fail(LGS_EINVAL, "bits_per_key %d out of range", bits_per_key);
   LGS_HIP(launch_bloom_build(d_keys, d_key_off, d_key_len, d_first, nfilters,
                              (uint32_t)bits_per_key, bloom_k(bits_per_key), d_out, d_out_off,
-                             (hipStream_t)stream));
+                             0, (hipStream_t)stream));
   return LGS_OK;
 }
 
@@ -831,7 +831,7 @@ int lgs_bloom_build_host(const uint8_t* keys, const uint64_t* key_off, const uin
   LGS_HIP(launch_bloom_build(d, (const uint64_t*)(d + o_koff), (const uint32_t*)(d + o_klen),
                              (const uint32_t*)(d + o_first), nfilters, (uint32_t)bits_per_key,
                              bloom_k(bits_per_key), d + o_filt, (const uint64_t*)(d + o_foff),
-                             c.stream));
+                             0, c.stream));
   LGS_HIP(hipMemcpyAsync(h + o_filt, d + o_filt, filt_bytes, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
   for (uint32_t f = 0; f < nfilters; ++f)
@@ -896,6 +896,210 @@ int lgs_bloom_match_host(const uint8_t* filters, const uint64_t* filter_off,
   LGS_HIP(launch_bloom_match(d + o_f, (const uint64_t*)(d + o_foff), (const uint32_t*)(d + o_flen),
                              (const uint32_t*)(d + o_qf), d + o_k, (const uint64_t*)(d + o_koff),
                              (const uint32_t*)(d + o_klen), d + o_m, nq, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_m, d + o_m, nq, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  memcpy(match, h + o_m, nq);
+  return LGS_OK;
+}
+
+// ---- the filter block (filter_block.c; kernels: lgs_bloom.hip) ----
+
+namespace {
+
+constexpr uint64_t kMaxDataEnd = 1ull << 42;   // 2^31 filters: offsets fit the u32 array
+
+struct FilterScratch {
+  size_t kf, foff, part, meta, total;
+  explicit FilterScratch(uint64_t data_end) {
+    const size_t nf = (size_t)(data_end >> 11) + 2;
+    Layout L;
+    kf = L.take(4 * nf);
+    foff = L.take(8 * nf);
+    part = L.take(8 * filter_block_parts(data_end));
+    meta = L.take(12);
+    total = L.at;
+  }
+};
+
+int filter_args(uint32_t nblocks, uint64_t data_end, int bits_per_key, int internal_keys) {
+  if (bits_per_key < 0 || bits_per_key > kMaxBitsPerKey)
+    return fail(LGS_EINVAL, "bits_per_key %d out of range", bits_per_key);
+  if (data_end >= kMaxDataEnd) return fail(LGS_EINVAL, "data_end %llu too large",
+                                           (unsigned long long)data_end);
+  if (internal_keys != 0 && internal_keys != 1)
+    return fail(LGS_EINVAL, "internal_keys must be 0 or 1");
+  (void)nblocks;
+  return LGS_OK;
+}
+
+}  // namespace
+
+size_t lgs_filter_block_bound(uint32_t nkeys, uint32_t nblocks, uint64_t data_end,
+                              int bits_per_key) {
+  if (bits_per_key < 0 || data_end >= kMaxDataEnd) return 0;
+  // Nonempty filters <= nblocks, each <= n * bpk / 8 + 10 bytes; 4 bytes per
+  // filter offset (<= data_end / 2048 + 1 of them), 5 trailing.
+  return (size_t)(((uint64_t)nkeys * (uint64_t)bits_per_key + 7) / 8 + 10ull * nblocks +
+                  4ull * ((data_end >> 11) + 1) + 5);
+}
+
+size_t lgs_filter_block_scratch(uint64_t data_end) {
+  if (data_end >= kMaxDataEnd) return 0;
+  return FilterScratch(data_end).total;
+}
+
+int lgs_filter_block_build_dev(const uint8_t* d_keys, const uint64_t* d_key_off,
+                               const uint32_t* d_key_len, uint32_t nkeys,
+                               const uint32_t* d_block_first, const uint64_t* d_block_off,
+                               uint32_t nblocks, uint64_t data_end, int bits_per_key,
+                               int internal_keys, uint8_t* d_out, size_t out_cap,
+                               uint64_t* d_size, void* d_scratch, size_t scratch_bytes,
+                               void* stream) {
+  LGS_TRY(filter_args(nblocks, data_end, bits_per_key, internal_keys));
+  if (!d_block_first || !d_out || !d_size || !d_scratch || (nblocks && !d_block_off) ||
+      (nkeys && (!d_keys || !d_key_off || !d_key_len)))
+    return fail(LGS_EINVAL, "NULL argument");
+  const FilterScratch S(data_end);
+  if (scratch_bytes < S.total)
+    return fail(LGS_EINVAL, "scratch %zu < %zu (lgs_filter_block_scratch)", scratch_bytes,
+                S.total);
+  const size_t bound = lgs_filter_block_bound(nkeys, nblocks, data_end, bits_per_key);
+  if (out_cap < bound)
+    return fail(LGS_ENOSPC, "out_cap %zu < %zu (lgs_filter_block_bound)", out_cap, bound);
+  uint8_t* sc = (uint8_t*)d_scratch;
+  LGS_HIP(launch_filter_block_build(d_keys, d_key_off, d_key_len, d_block_first, d_block_off,
+                                    nblocks, data_end, (uint32_t)bits_per_key,
+                                    bloom_k(bits_per_key), internal_keys ? 8u : 0u, d_out,
+                                    d_size, (uint32_t*)(sc + S.kf), (uint64_t*)(sc + S.foff),
+                                    (uint64_t*)(sc + S.part), (uint32_t*)(sc + S.meta),
+                                    (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_filter_block_build_host(const uint8_t* keys, const uint64_t* key_off,
+                                const uint32_t* key_len, const uint32_t* block_first,
+                                const uint64_t* block_off, uint32_t nblocks, uint64_t data_end,
+                                int bits_per_key, int internal_keys, uint8_t* out,
+                                size_t out_cap, size_t* size) {
+  LGS_TRY(filter_args(nblocks, data_end, bits_per_key, internal_keys));
+  if (!block_first || !out || !size || (nblocks && !block_off))
+    return fail(LGS_EINVAL, "NULL argument");
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    if (block_first[b + 1] < block_first[b])
+      return fail(LGS_EINVAL, "block_first[] decreases at block %u", b);
+    if ((b + 1 < nblocks ? block_off[b + 1] : data_end) < block_off[b])
+      return fail(LGS_EINVAL, "block offsets decrease at block %u", b);
+  }
+  const uint32_t k0 = block_first[0], nkeys = block_first[nblocks] - k0;
+  if (nkeys && (!keys || !key_off || !key_len)) return fail(LGS_EINVAL, "NULL argument");
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  size_t key_bytes = 0;
+  for (uint32_t i = k0; i < k0 + nkeys; ++i) key_bytes += key_len[i];
+  const size_t bound = lgs_filter_block_bound(nkeys, nblocks, data_end, bits_per_key);
+  const FilterScratch S(data_end);
+  Layout L;  // upload | scratch | download
+  const size_t o_keys = L.take(key_bytes + 16);
+  const size_t o_koff = L.take(8 * (size_t)nkeys);
+  const size_t o_klen = L.take(4 * (size_t)nkeys);
+  const size_t o_bf = L.take(4 * ((size_t)nblocks + 1));
+  const size_t o_bo = L.take(8 * (size_t)nblocks);
+  const size_t up_end = L.at;
+  const size_t o_scr = L.take(S.total);
+  const size_t o_size = L.take(8);
+  const size_t o_out = L.take(bound);
+  const size_t down_end = o_out + bound;
+  LGS_TRY(ctx_reserve(c, L.at, L.at));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  uint64_t* koff = (uint64_t*)(h + o_koff);
+  uint32_t* klen = (uint32_t*)(h + o_klen);
+  uint32_t* bf = (uint32_t*)(h + o_bf);
+  size_t at = o_keys;
+  for (uint32_t j = 0; j < nkeys; ++j) {
+    memcpy(h + at, keys + key_off[k0 + j], key_len[k0 + j]);
+    koff[j] = at;
+    klen[j] = key_len[k0 + j];
+    at += key_len[k0 + j];
+  }
+  memset(h + at, 0, 16);
+  for (uint32_t b = 0; b <= nblocks; ++b) bf[b] = block_first[b] - k0;
+  if (nblocks) memcpy(h + o_bo, block_off, 8 * (size_t)nblocks);
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  LGS_TRY(lgs_filter_block_build_dev(d, (const uint64_t*)(d + o_koff),
+                                     (const uint32_t*)(d + o_klen), nkeys,
+                                     (const uint32_t*)(d + o_bf), (const uint64_t*)(d + o_bo),
+                                     nblocks, data_end, bits_per_key, internal_keys, d + o_out,
+                                     bound, (uint64_t*)(d + o_size), d + o_scr, S.total,
+                                     c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_size, d + o_size, down_end - o_size, hipMemcpyDeviceToHost,
+                         c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint64_t n = *(const uint64_t*)(h + o_size);
+  if (n > bound) return fail(LGS_EINTERNAL, "filter block %llu > bound %zu",
+                             (unsigned long long)n, bound);
+  *size = (size_t)n;
+  if (n > out_cap) return fail(LGS_ENOSPC, "filter block needs %llu bytes, out_cap %zu",
+                               (unsigned long long)n, out_cap);
+  memcpy(out, h + o_out, (size_t)n);
+  return LGS_OK;
+}
+
+int lgs_filter_block_match_dev(const uint8_t* d_block, size_t block_len,
+                               const uint64_t* d_block_offset, const uint8_t* d_keys,
+                               const uint64_t* d_key_off, const uint32_t* d_key_len, uint32_t nq,
+                               int internal_keys, uint8_t* d_match, void* stream) {
+  if (nq == 0) return LGS_OK;
+  if ((block_len && !d_block) || !d_block_offset || !d_keys || !d_key_off || !d_key_len ||
+      !d_match)
+    return fail(LGS_EINVAL, "NULL argument");
+  if (internal_keys != 0 && internal_keys != 1)
+    return fail(LGS_EINVAL, "internal_keys must be 0 or 1");
+  LGS_HIP(launch_filter_block_match(d_block, block_len, d_block_offset, d_keys, d_key_off,
+                                    d_key_len, internal_keys ? 8u : 0u, d_match, nq,
+                                    (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_filter_block_match_host(const uint8_t* block, size_t block_len,
+                                const uint64_t* block_offset, const uint8_t* keys,
+                                const uint64_t* key_off, const uint32_t* key_len, uint32_t nq,
+                                int internal_keys, uint8_t* match) {
+  if (nq == 0) return LGS_OK;
+  if ((block_len && !block) || !block_offset || !keys || !key_off || !key_len || !match)
+    return fail(LGS_EINVAL, "NULL argument");
+  Ctx& c = t_ctx;
+  LGS_TRY(ctx_ready(c));
+  size_t kb = 0;
+  for (uint32_t q = 0; q < nq; ++q) kb += key_len[q];
+  Layout L;
+  const size_t o_b = L.take(block_len + 16);
+  const size_t o_qo = L.take(8 * (size_t)nq);
+  const size_t o_k = L.take(kb + 16);
+  const size_t o_koff = L.take(8 * (size_t)nq);
+  const size_t o_klen = L.take(4 * (size_t)nq);
+  const size_t up_end = L.at;
+  const size_t o_m = L.take(nq);
+  LGS_TRY(ctx_reserve(c, L.at, L.at));
+  uint8_t* h = c.h_buf;
+  uint8_t* d = c.d_buf;
+  if (block_len) memcpy(h + o_b, block, block_len);
+  memcpy(h + o_qo, block_offset, 8 * (size_t)nq);
+  uint64_t* koff = (uint64_t*)(h + o_koff);
+  uint32_t* klen = (uint32_t*)(h + o_klen);
+  size_t at = 0;
+  for (uint32_t q = 0; q < nq; ++q) {
+    memcpy(h + o_k + at, keys + key_off[q], key_len[q]);
+    koff[q] = at;
+    klen[q] = key_len[q];
+    at += key_len[q];
+  }
+  memset(h + o_k + at, 0, 16);
+  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+  LGS_TRY(lgs_filter_block_match_dev(d + o_b, block_len, (const uint64_t*)(d + o_qo), d + o_k,
+                                     (const uint64_t*)(d + o_koff),
+                                     (const uint32_t*)(d + o_klen), nq, internal_keys, d + o_m,
+                                     c.stream));
   LGS_HIP(hipMemcpyAsync(h + o_m, d + o_m, nq, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
   memcpy(match, h + o_m, nq);

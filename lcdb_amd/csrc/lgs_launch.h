@@ -72,16 +72,34 @@ hipError_t launch_merge(uint8_t* status, uint32_t* out_len, const uint8_t* dec_s
 // ---- bloom filter (lgs_bloom.hip) ----
 
 // Filters f = keys [first[f], first[f+1]) written at out + out_off[f]
-// (bloom.c:102-119); bpk = bits per key, k = probes (bloom.c:35-45).
+// (bloom.c:102-119); bpk = bits per key, k = probes (bloom.c:35-45); each
+// key hashed without its last `trim` bytes (8: the internal filter policy).
 hipError_t launch_bloom_build(const uint8_t* keys, const uint64_t* key_off,
                               const uint32_t* key_len, const uint32_t* first, uint32_t nfilters,
                               uint32_t bpk, uint32_t k, uint8_t* out, const uint64_t* out_off,
-                              hipStream_t s);
+                              uint32_t trim, hipStream_t s);
 // match[q] = bloom_match(filter qfilter[q], key q) (bloom.c:121-165).
 hipError_t launch_bloom_match(const uint8_t* filters, const uint64_t* filter_off,
                               const uint32_t* filter_len, const uint32_t* qfilter,
                               const uint8_t* keys, const uint64_t* key_off,
                               const uint32_t* key_len, uint8_t* match, uint32_t nq,
                               hipStream_t s);
+// The filter block of one table (filter_block.c:79-150 as table_builder.c
+// drives it): data block b = keys [block_first[b], block_first[b+1]) at file
+// offset block_off[b]; data_end = offset after the last one.  Scratch: kf
+// (fmax + 1 u32), foff (fmax + 1 u64), meta (1 u32), fmax = data_end/2048 + 1.
+// out receives the block, size[0] its length.
+hipError_t launch_filter_block_build(const uint8_t* keys, const uint64_t* key_off,
+                                     const uint32_t* key_len, const uint32_t* block_first,
+                                     const uint64_t* block_off, uint32_t nblocks,
+                                     uint64_t data_end, uint32_t bpk, uint32_t k, uint32_t trim,
+                                     uint8_t* out, uint64_t* size, uint32_t* kf, uint64_t* foff,
+                                     uint64_t* part, uint32_t* meta, hipStream_t s);
+size_t filter_block_parts(uint64_t data_end);
+// match[q] = ldb_filter_matches(block, qoff[q], key q) (filter_block.c:170-225).
+hipError_t launch_filter_block_match(const uint8_t* blk, uint64_t n, const uint64_t* qoff,
+                                     const uint8_t* keys, const uint64_t* key_off,
+                                     const uint32_t* key_len, uint32_t trim, uint8_t* match,
+                                     uint32_t nq, hipStream_t s);
 
 }  // namespace lgs

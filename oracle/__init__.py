@@ -258,6 +258,15 @@ class Bloom:
         self.f_build.argtypes = [vp, vp, vp, sz, C.c_int, vp] + ([sz] if with_cap else [])
         self.f_match = getattr(d, match_fn)
         self.f_match.restype, self.f_match.argtypes = C.c_int, [vp, sz, vp, sz]
+        pre = "ref" if with_cap else "oracle"
+        self.f_fb = getattr(d, pre + "_filter_block_build")
+        self.f_fb.restype = sz
+        self.f_fb.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint64, C.c_int,
+                              C.c_int if with_cap else C.c_uint32, vp,
+                              sz if with_cap else vp]
+        self.f_fm = getattr(d, pre + "_filter_matches")
+        self.f_fm.restype = C.c_int
+        self.f_fm.argtypes = [vp, sz, C.c_uint64, vp, sz, C.c_int if with_cap else C.c_uint32]
 
     def hash(self, data: bytes, seed: int) -> int:
         b = _buf(data)
@@ -279,6 +288,42 @@ class Bloom:
     def match(self, filt: bytes, key: bytes) -> bool:
         f, k = _buf(filt), _buf(key)
         return bool(self.f_match(f.ctypes.data, len(filt), k.ctypes.data, len(key)))
+
+    # -- the filter block (filter_block.c), see oracle_filter_block_build --
+    def filter_block(self, blocks, block_off, data_end: int, bits_per_key: int = 10,
+                     internal: bool = False) -> bytes:
+        """blocks[b] = the keys of data block b (file order); block_off[b] =
+        its file offset; data_end = the offset after the last data block."""
+        keys = [k for blk in blocks for k in blk]
+        lens = np.array([len(k) for k in keys], dtype=np.uint32)
+        offs = np.zeros(len(keys), dtype=np.uint64)
+        if len(keys):
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        base = np.frombuffer(b"".join(keys) + b"\0" * 8, dtype=np.uint8)
+        first = np.zeros(len(blocks) + 1, dtype=np.uint32)
+        first[1:] = np.cumsum([len(b) for b in blocks], dtype=np.uint64)
+        boff = np.array(list(block_off) + [0], dtype=np.uint64)
+        nf = data_end // 2048 + 2
+        cap = len(keys) * max(bits_per_key, 0) // 8 + 10 * (len(blocks) + 1) + 4 * nf + 64
+        out = np.zeros(cap, dtype=np.uint8)
+        if self.with_cap:
+            n = self.f_fb(base.ctypes.data, offs.ctypes.data, lens.ctypes.data, first.ctypes.data,
+                          boff.ctypes.data, len(blocks), data_end, bits_per_key, int(internal),
+                          out.ctypes.data, cap)
+        else:
+            scratch = np.zeros(nf, dtype=np.uint32)
+            n = self.f_fb(base.ctypes.data, offs.ctypes.data, lens.ctypes.data, first.ctypes.data,
+                          boff.ctypes.data, len(blocks), data_end, bits_per_key,
+                          8 if internal else 0, out.ctypes.data, scratch.ctypes.data)
+        assert n > 0
+        return out[:n].tobytes()
+
+    def filter_matches(self, block: bytes, block_offset: int, key: bytes,
+                       internal: bool = False) -> bool:
+        f, k = _buf(block), _buf(key)
+        flag = int(internal) if self.with_cap else (8 if internal else 0)
+        return bool(self.f_fm(f.ctypes.data, len(block), block_offset, k.ctypes.data, len(key),
+                              flag))
 
 
 _bloom_orc = None

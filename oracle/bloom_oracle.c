@@ -7,7 +7,10 @@
  *   - the builtin bloom policy (src/util/bloom.c:24-165): k from
  *     bits_per_key (:35-45), filter size (:69-80), the double-hashed probes
  *     of bloom_add (:82-100), bloom_build (:102-119: bits, then one byte k)
- *     and bloom_match (:121-165).
+ *     and bloom_match (:121-165);
+ *   - the filter block (src/table/filter_block.c:79-225): one filter per
+ *     2 KiB of data-block offsets, built the way the table builder drives it
+ *     (table_builder.c:242-243, 276-277, 294), and ldb_filter_matches.
  * Nothing in lcdb_amd/ links, loads or calls this file.
  *
  * Parity pin: the known answers of test/t-hash.c:33-38, and filters built
@@ -17,6 +20,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "bloom_oracle.h"
@@ -118,5 +122,99 @@ oracle_bloom_match(const uint8_t *filter, size_t len, const uint8_t *key, size_t
       return 0;
     h += delta;
   }
+  return 1;
+}
+
+/* ---- the filter block (src/table/filter_block.c) ---- */
+
+static void
+orc_put32(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  p[2] = (uint8_t)(v >> 16);
+  p[3] = (uint8_t)(v >> 24);
+}
+
+/* The filter block of one table, as lcdb's table builder makes it: for each
+   data block b in file order, its keys [block_first[b], block_first[b + 1])
+   go to ldb_filtergen_add_key (table_builder.c:242-243), then the block is
+   written and ldb_filtergen_start_block(offset after the block) runs
+   (table_builder.c:276-277); ldb_filtergen_finish (table_builder.c:294) at the
+   end.  The offset after block b is block_off[b + 1] (data_end for the last).
+   filter_block.c:79-150 restated: `generate` turns the pending keys into one
+   filter (or an empty one) and records its offset; start_block generates
+   until there is one filter per started 2 KiB (LDB_FILTER_BASE_LG = 11).
+   trim = 8 restates the internal filter policy (dbformat.c:308-326: user key
+   = key without its 8-byte trailer).  Writes to out (no bound check: size it
+   with oracle_filter_block_bound) and returns the size. */
+size_t
+oracle_filter_block_build(const uint8_t *base, const uint64_t *key_off, const uint32_t *key_len,
+                          const uint32_t *block_first, const uint64_t *block_off,
+                          uint32_t nblocks, uint64_t data_end, int bits_per_key, uint32_t trim,
+                          uint8_t *out, uint32_t *filter_offsets) {
+  size_t result = 0;          /* bytes of filters so far */
+  uint32_t nfilt = 0;         /* filter_offsets.length */
+  uint32_t pend0 = 0, pend1 = 0;   /* pending keys [pend0, pend1) */
+  uint32_t b, f;
+
+  for (b = 0; b <= nblocks; b++) {
+    uint64_t end, index;
+    if (b < nblocks) {
+      pend1 = block_first[b + 1];            /* add_key for the block's keys */
+      end = b + 1 < nblocks ? block_off[b + 1] : data_end;
+      index = end >> 11;                     /* start_block, :114-121 */
+    } else {
+      index = 0;                             /* finish, :131-150 */
+      if (pend1 > pend0)
+        index = (uint64_t)nfilt + 1;
+    }
+    while (index > nfilt) {                  /* generate, :79-112 */
+      filter_offsets[nfilt++] = (uint32_t)result;
+      if (pend1 > pend0) {
+        size_t n = pend1 - pend0, i;
+        uint64_t *o = (uint64_t *)malloc(n * sizeof(uint64_t));
+        uint32_t *l = (uint32_t *)malloc(n * sizeof(uint32_t));
+        for (i = 0; i < n; i++) {
+          o[i] = key_off[pend0 + i];
+          l[i] = key_len[pend0 + i] > trim ? key_len[pend0 + i] - trim : 0;
+        }
+        result += oracle_bloom_build(base, o, l, n, bits_per_key, out + result);
+        free(o);
+        free(l);
+        pend0 = pend1;
+      }
+    }
+  }
+  for (f = 0; f < nfilt; f++)
+    orc_put32(out + result + 4 * f, filter_offsets[f]);
+  orc_put32(out + result + 4 * nfilt, (uint32_t)result);
+  out[result + 4 * nfilt + 4] = 11;          /* LDB_FILTER_BASE_LG */
+  return result + 4 * (size_t)nfilt + 5;
+}
+
+/* ldb_filter_init + ldb_filter_matches (filter_block.c:170-225) for the key
+   of a data block at block_offset; trim as above (ldb_ifp_match,
+   dbformat.c:328-334). */
+int
+oracle_filter_matches(const uint8_t *block, size_t n, uint64_t block_offset,
+                      const uint8_t *key, size_t klen, uint32_t trim) {
+  uint32_t base_lg, last_word, start, limit;
+  uint64_t index, num;
+  if (n < 5)
+    return 1;                                /* num = 0 */
+  base_lg = block[n - 1] & 63;
+  last_word = orc_le32(block + n - 5);
+  if (last_word > n - 5)
+    return 1;
+  num = (n - 5 - last_word) / 4;
+  index = block_offset >> base_lg;
+  if (index >= num)
+    return 1;
+  start = orc_le32(block + last_word + index * 4);
+  limit = orc_le32(block + last_word + index * 4 + 4);
+  if (start <= limit && limit <= last_word)
+    return oracle_bloom_match(block + start, limit - start, key, klen > trim ? klen - trim : 0);
+  if (start == limit)
+    return 0;
   return 1;
 }

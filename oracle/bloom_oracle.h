@@ -15,4 +15,12 @@ size_t oracle_bloom_build(const uint8_t *base, const uint64_t *off, const uint32
                           size_t n, int bits_per_key, uint8_t *out);
 int oracle_bloom_match(const uint8_t *filter, size_t len, const uint8_t *key, size_t klen);
 
+size_t oracle_filter_block_build(const uint8_t *base, const uint64_t *key_off,
+                                 const uint32_t *key_len, const uint32_t *block_first,
+                                 const uint64_t *block_off, uint32_t nblocks, uint64_t data_end,
+                                 int bits_per_key, uint32_t trim, uint8_t *out,
+                                 uint32_t *filter_offsets);
+int oracle_filter_matches(const uint8_t *block, size_t n, uint64_t block_offset,
+                          const uint8_t *key, size_t klen, uint32_t trim);
+
 #endif

@@ -15,7 +15,11 @@
  * sequence k + 1, 100-byte values from the db_bench value generator
  * (seed 301, ratio 0.5; db_bench.c:206-246 via src/util/testutil.c).
  *
- * usage: build_table DIR NUM_ENTRIES [BLOCK_SIZE]
+ * With BLOOM_BITS > 0 the table also gets lcdb's filter block: the DB's
+ * internal filter policy (dbformat.c:308-345) over ldb_bloom_init(BLOOM_BITS),
+ * as db_impl.c:455-460 sets it up.
+ *
+ * usage: build_table DIR NUM_ENTRIES [BLOCK_SIZE [BLOOM_BITS]]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -27,6 +31,7 @@
 #include "table_cache.h"
 #include "version_edit.h"
 #include "table/iterator.h"
+#include "util/bloom.h"
 #include "util/buffer.h"
 #include "util/comparator.h"
 #include "util/env.h"
@@ -48,11 +53,12 @@ main(int argc, char **argv) {
   ldb_iter_t *iter;
   ldb_buffer_t ring, piece;
   ldb_rand_t rnd;
+  ldb_bloom_t user_bloom, ifp;
   size_t pos = 0;
   int rc;
 
   if (argc < 3) {
-    fprintf(stderr, "usage: %s DIR NUM_ENTRIES [BLOCK_SIZE]\n", argv[0]);
+    fprintf(stderr, "usage: %s DIR NUM_ENTRIES [BLOCK_SIZE [BLOOM_BITS]]\n", argv[0]);
     return 2;
   }
 
@@ -64,6 +70,11 @@ main(int argc, char **argv) {
   options.comparator = &icmp;
   if (argc > 3)
     options.block_size = (size_t)atol(argv[3]);
+  if (argc > 4 && atoi(argv[4]) > 0) {
+    ldb_bloom_init(&user_bloom, atoi(argv[4]));
+    ldb_ifp_init(&ifp, &user_bloom);
+    options.filter_policy = &ifp;
+  }
 
   ldb_create_dir(dir);
 

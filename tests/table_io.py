@@ -37,11 +37,14 @@ def binary(name: str) -> str:
     return p
 
 
-def build_table(tmp, entries: int, block_size: int, kind: str = "cpu") -> str:
-    """An .ldb of db_bench fillseq entries written by lcdb's own builder."""
-    d = os.path.join(str(tmp), f"db_{kind}_{entries}_{block_size}")
-    r = subprocess.run([binary(f"build_table.{kind}"), d, str(entries), str(block_size)],
-                       capture_output=True, text=True, timeout=600)
+def build_table(tmp, entries: int, block_size: int, kind: str = "cpu", bloom_bits: int = 0) -> str:
+    """An .ldb of db_bench fillseq entries written by lcdb's own builder
+    (with its filter block when bloom_bits > 0)."""
+    d = os.path.join(str(tmp), f"db_{kind}_{entries}_{block_size}_{bloom_bits}")
+    args = [binary(f"build_table.{kind}"), d, str(entries), str(block_size)]
+    if bloom_bits:
+        args.append(str(bloom_bits))
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "rc=0" in r.stdout, r.stdout + r.stderr
     return os.path.join(d, "000001.ldb")
 
@@ -94,3 +97,53 @@ def corrupt(data: bytes, lo: int, hi: int, count: int, seed: int) -> bytes:
     for p in rng.integers(lo, hi, size=count):
         b[int(p)] ^= int(rng.integers(1, 256))
     return bytes(b)
+
+
+def _varint(b: bytes, at: int, limit: int, bits: int):
+    """coding.h varint32/64 read: (value, next) or None."""
+    v, sh = 0, 0
+    while at < limit and sh <= bits - 1:
+        c = b[at]
+        at += 1
+        v |= (c & 0x7F) << sh
+        if c < 0x80:
+            return v, at
+        sh += 7
+    return None
+
+
+def block_entries(contents: bytes) -> list[tuple[bytes, bytes]]:
+    """A block's (key, value) entries in order, as lcdb's block iterator
+    walks them from the first restart (block.c:49-130, 255-297).  Test
+    helper: asserts on malformed blocks."""
+    n = len(contents)
+    assert n >= 4
+    nr = struct.unpack_from("<I", contents, n - 4)[0]
+    assert nr <= (n - 4) // 4
+    limit = n - (1 + nr) * 4
+    out, key, at = [], b"", 0
+    while at < limit:
+        if limit - at >= 3 and max(contents[at:at + 3]) < 128:
+            shared, non_shared, vlen = contents[at], contents[at + 1], contents[at + 2]
+            at += 3
+        else:
+            shared, at = _varint(contents, at, limit, 32)
+            non_shared, at = _varint(contents, at, limit, 32)
+            vlen, at = _varint(contents, at, limit, 32)
+        assert shared <= len(key) and at + non_shared + vlen <= limit
+        key = key[:shared] + contents[at:at + non_shared]
+        at += non_shared
+        out.append((key, contents[at:at + vlen]))
+        at += vlen
+    return out
+
+
+def filter_handle(metaindex: bytes, name: bytes = b"filter.leveldb.BuiltinBloomFilter2"):
+    """(offset, size) of the filter block named in a metaindex block
+    (table.c:78-120), or None."""
+    for k, v in block_entries(metaindex):
+        if k == name:
+            off, at = _varint(v, 0, len(v), 64)
+            size, _ = _varint(v, at, len(v), 64)
+            return off, size
+    return None

@@ -80,3 +80,95 @@ def test_members_always_match():
     for g in key_groups(3):
         f = orc.build(g, 10)
         assert all(orc.match(f, k) for k in g)
+
+
+# ---- the filter block (filter_block.c) ----
+
+def random_table_layout(rng: random.Random, internal: bool):
+    """Data blocks of random keys at increasing file offsets, the shapes the
+    filter block meets: empty tables, blocks under and over 2 KiB, a first
+    block not at offset 0, key-less blocks (never written by lcdb, but the
+    builder's arithmetic is defined for them)."""
+    nb = rng.randrange(0, 12)
+    lo = 8 if internal else 0
+    blocks = [[rng.randbytes(rng.randrange(lo, 30)) for _ in range(
+        rng.randrange(0 if rng.random() < 0.1 else 1, 40))] for _ in range(nb)]
+    off, pos = [], rng.choice([0, 0, 0, 3000])
+    for _ in blocks:
+        off.append(pos)
+        pos += rng.choice([rng.randrange(10, 300), rng.randrange(100, 9000)])
+    return blocks, off, pos
+
+
+def test_filter_block_vs_reference():
+    ref = oracle.bloom_reference()
+    if ref is None:
+        pytest.skip("oracle/_ref/lcdb/libref_bloom.so not built")
+    orc = oracle.bloom_restatement()
+    rng = random.Random(21)
+    for _ in range(150):
+        internal = rng.random() < 0.5
+        blocks, off, end = random_table_layout(rng, internal)
+        bpk = rng.choice([1, 10, 16])
+        fb = orc.filter_block(blocks, off, end, bpk, internal)
+        assert fb == ref.filter_block(blocks, off, end, bpk, internal), (off, end)
+        keys = [k for b in blocks for k in b] or [b"x" * 9]
+        for _ in range(20):
+            bo = rng.randrange(0, end + 5000)
+            key = rng.choice(keys) if rng.random() < 0.5 else rng.randbytes(rng.randrange(8, 20))
+            assert orc.filter_matches(fb, bo, key, internal) == ref.filter_matches(fb, bo, key,
+                                                                                   internal)
+
+
+def malformed_filter_blocks(rng: random.Random, count: int):
+    """Too-short blocks, offset arrays past the end, inverted ranges."""
+    out = []
+    for _ in range(count):
+        b = bytearray(rng.randbytes(rng.randrange(0, 40)))
+        if len(b) >= 5 and rng.random() < 0.7:
+            b[-5:-1] = rng.randrange(0, len(b)).to_bytes(4, "little")
+            b[-1] = rng.choice([11, 0, 63, 200])
+        out.append(bytes(b))
+    return out
+
+
+def test_filter_matches_malformed_vs_reference():
+    ref = oracle.bloom_reference()
+    if ref is None:
+        pytest.skip("oracle/_ref/lcdb/libref_bloom.so not built")
+    orc = oracle.bloom_restatement()
+    rng = random.Random(5)
+    for blk in malformed_filter_blocks(rng, 1500):
+        bo, key = rng.randrange(0, 1 << 16), rng.randbytes(rng.randrange(8, 12))
+        for internal in (False, True):
+            assert orc.filter_matches(blk, bo, key, internal) == \
+                ref.filter_matches(blk, bo, key, internal), (blk, bo)
+
+
+def lcdb_table_with_filter(tmp_path, entries=5000, block_size=4096):
+    """An .ldb written by lcdb's own builder with the DB's filter policy
+    (bloom, 10 bits/key), its data blocks' keys and offsets, and its filter
+    block as stored in the file."""
+    from table_io import block_entries, build_table, dump_blocks, filter_handle
+    path = build_table(tmp_path, entries, block_size, bloom_bits=10)
+    d = dump_blocks(path, str(tmp_path / "dump"), True)
+    nd = d.n - 2                                   # data blocks, then metaindex, index
+    fh = filter_handle(d.contents[-2])
+    assert fh is not None
+    raw = open(path, "rb").read()
+    blocks = [[k for k, _ in block_entries(c)] for c in d.contents[:nd]]
+    off = [int(x) for x in d.off[:nd]]
+    data_end = int(d.off[nd - 1] + d.size[nd - 1] + 5)
+    assert fh[0] == data_end                      # the filter block follows the data
+    return blocks, off, data_end, raw[fh[0]:fh[0] + fh[1]]
+
+
+def test_filter_block_of_lcdb_table(tmp_path):
+    """The restatement reproduces the filter block lcdb's table builder wrote
+    (internal keys, user-key filters), and it answers every key present."""
+    blocks, off, end, stored = lcdb_table_with_filter(tmp_path)
+    orc = oracle.bloom_restatement()
+    assert orc.filter_block(blocks, off, end, 10, True) == stored
+    for b, keys in enumerate(blocks):
+        for k in keys[::7]:
+            assert orc.filter_matches(stored, off[b], k, True)
