@@ -179,6 +179,31 @@ int lgs_table_read_host(const uint8_t *file, uint64_t file_len,
                         const uint64_t *out_off, const uint32_t *out_cap,
                         uint32_t *out_len, uint8_t *status);
 
+/* Row 3, opening a table: ldb_table_open (table.c:120-180) and the index
+   walk of its two-level iterator, for the batched read above.  From the
+   footer (format.c:116-137) it reads the index block through
+   lgs_table_read_host (checksums verified when paranoid_checks, as
+   table.c:148-151) and returns, in index order, each entry's data-block
+   handle (handle_off/handle_size, cap of them; *count written) and, if keys
+   != NULL, its separator key (keys[key_off[i] .. key_off[i+1]), keys_cap
+   bytes, key_off has cap + 1 entries).  internal_keys: index keys are
+   internal keys (the DB's tables), so one under 8 bytes is a bad entry
+   (block.c:270-273).  With filter_name (e.g.
+   "filter.leveldb.BuiltinBloomFilter2") the metaindex is read too and
+   *filter_off and *filter_size receive that entry's handle, or ~0 / 0 when
+   there is none or the metaindex does not read (table.c:78-120 ignores
+   those errors).  *status: LGS_ST_OK; LGS_ST_CORRUPT for a short file, a
+   bad footer, a bad index block or entry (the walk stops there), or an
+   entry whose value is no handle (skipped, as the two-level iterator skips
+   it); the block read's own status (LGS_ST_IOERR, _BADCRC, _BADTYPE) when
+   the index block does not read.  Returns LGS_ENOSPC when cap or keys_cap is
+   too small. */
+int lgs_table_index_host(const uint8_t *file, uint64_t file_len, int paranoid_checks,
+                         int internal_keys, const char *filter_name, uint64_t *handle_off,
+                         uint64_t *handle_size, uint32_t cap, uint32_t *count, uint8_t *keys,
+                         size_t keys_cap, uint64_t *key_off, uint64_t *filter_off,
+                         uint64_t *filter_size, uint8_t *status);
+
 /* Row 4.  lcdb's builtin bloom filter (src/util/bloom.c, src/util/hash.c):
    filter f holds keys [first[f], first[f+1]) and is written at out +
    out_off[f] exactly as ldb_bloom_build appends it (bloom.c:102-119):

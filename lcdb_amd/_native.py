@@ -42,6 +42,8 @@ _SIGS = {
                                      _vp, C.c_uint32, _vp, _vp, _vp, C.c_size_t, _vp]),
     "lgs_table_read_host": (C.c_int, [_vp, C.c_uint64, _vp, _vp, C.c_uint32, C.c_int, _vp, _vp,
                                       _vp, _vp, _vp]),
+    "lgs_table_index_host": (C.c_int, [_vp, C.c_uint64, C.c_int, C.c_int, C.c_char_p, _vp, _vp,
+                                       C.c_uint32, _vp, _vp, C.c_size_t, _vp, _vp, _vp, _vp]),
     "lgs_bloom_filter_size": (C.c_size_t, [C.c_uint32, C.c_int]),
     "lgs_bloom_build_dev": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint32, C.c_int, _vp, _vp, _vp]),
     "lgs_bloom_match_dev": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_uint32, _vp]),

@@ -275,6 +275,9 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
 }
 
 }  // namespace
+
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
 }  // namespace lgs
 
 using namespace lgs;

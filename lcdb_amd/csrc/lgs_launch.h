@@ -102,4 +102,7 @@ hipError_t launch_filter_block_match(const uint8_t* blk, uint64_t n, const uint6
                                      const uint32_t* key_len, uint32_t trim, uint8_t* match,
                                      uint32_t nq, hipStream_t s);
 
+// Host runtime (lgs_api.cpp): record msg as lgs_last_error(); returns code.
+int set_error(int code, const char* msg);
+
 }  // namespace lgs

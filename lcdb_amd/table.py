@@ -11,7 +11,10 @@ the batched C ABI that does both for many blocks per launch
   (src/table/table_builder.c:123-213): encode, 12.5 % rule, trailer, packing;
 * ``read_blocks``     -- ``ldb_read_block`` for n handles
   (src/table/format.c:162-270): truncation, checksum, type, raw or decode;
-* ``*_host`` variants on host bytes (pinned staging inside the library).
+* ``*_host`` variants on host bytes (pinned staging inside the library);
+* ``index_host``      -- ``ldb_table_open``'s footer, index-block handles and
+  metaindex filter handle (src/table/table.c:78-180), the handles the batched
+  read takes.
 
 Everything runs through ``liblcdb_gpu_snappy.so``; there is no CPU fallback.
 """
@@ -31,6 +34,7 @@ _L = _native.lib()
 
 __all__ = [
     "crc32c_batch", "write_blocks", "read_blocks", "write_blocks_host", "read_blocks_host",
+    "index_host", "FILTER_NAME",
     "LGS_NO_COMPRESSION", "LGS_SNAPPY_COMPRESSION", "LGS_TRAILER_SIZE", "LGS_ST_OK",
     "LGS_ST_CORRUPT", "LGS_ST_NOSPACE", "LGS_ST_IOERR", "LGS_ST_BADCRC", "LGS_ST_BADTYPE",
 ]
@@ -157,3 +161,35 @@ def read_blocks_host(file, handle_off, handle_size, caps, verify: bool = True):
     res = [out[int(o):int(o) + int(k)].tobytes() if s == LGS_ST_OK else None
            for o, k, s in zip(ooff, olen, st)]
     return res, st
+
+
+FILTER_NAME = "filter.leveldb.BuiltinBloomFilter2"   # "filter." + bloom.c's policy name
+
+
+def index_host(file, paranoid_checks: bool = False, internal_keys: bool = False,
+               filter_name: str | None = FILTER_NAME, cap: int | None = None):
+    """ldb_table_open's view of a table file (lgs_table_index_host): returns
+    (handles [(offset, size)], separator keys, filter handle or None, status)."""
+    import ctypes as C
+    raw = bytes(file)
+    img = np.frombuffer(raw + b"\0", dtype=np.uint8)
+    cap = cap if cap is not None else max(1, len(raw) // 8)
+    hoff = np.zeros(cap, dtype=np.uint64)
+    hsize = np.zeros(cap, dtype=np.uint64)
+    keys = np.zeros(max(1, len(raw)), dtype=np.uint8)
+    koff = np.zeros(cap + 1, dtype=np.uint64)
+    count = C.c_uint32(0)
+    foff, fsize = C.c_uint64(0), C.c_uint64(0)
+    st = C.c_uint8(0)
+    check(_L.lgs_table_index_host(img.ctypes.data, len(raw), int(paranoid_checks),
+                                  int(internal_keys),
+                                  filter_name.encode() if filter_name else None,
+                                  hoff.ctypes.data, hsize.ctypes.data, cap, C.byref(count),
+                                  keys.ctypes.data, len(keys), koff.ctypes.data, C.byref(foff),
+                                  C.byref(fsize), C.byref(st)),
+          "lgs_table_index_host")
+    n = count.value
+    handles = [(int(hoff[i]), int(hsize[i])) for i in range(n)]
+    ks = [keys[int(koff[i]):int(koff[i + 1])].tobytes() for i in range(n)]
+    fh = None if foff.value == (1 << 64) - 1 else (foff.value, fsize.value)
+    return handles, ks, fh, st.value

@@ -206,6 +206,68 @@ def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path):
     assert list(st) == [tab.LGS_ST_BADTYPE, tab.LGS_ST_CORRUPT, tab.LGS_ST_NOSPACE]
 
 
+@pytest.mark.parametrize("bs", [4096, 256, 65536])
+def test_table_index_then_batched_read(tab, ref_tables, bs):
+    """ldb_table_open's view (footer -> index block -> data-block handles and
+    separator keys) matches the reference's index walk; the batched read of
+    those handles returns every data block as ldb_read_block does."""
+    path, file, d = ref_tables[bs]
+    ndata = d.n - 2
+    for paranoid in (True, False):
+        handles, keys, fh, st = tab.index_host(file, paranoid, internal_keys=True)
+        assert st == tab.LGS_ST_OK and fh is None       # no filter policy in these tables
+        assert handles == list(zip(d.off[:ndata].tolist(), d.size[:ndata].tolist()))
+        assert keys == [k for k, _ in table_io.block_entries(d.contents[-1])]
+    off = np.array([h[0] for h in handles], dtype=np.uint64)
+    size = np.array([h[1] for h in handles], dtype=np.uint64)
+    res, st = tab.read_blocks_host(file, off, size, [max(len(x), 1) for x in d.contents[:ndata]])
+    assert all(int(x) == tab.LGS_ST_OK for x in st)
+    assert res == d.contents[:ndata]
+
+
+def test_table_index_filter_handle(tab, tmp_path):
+    path = table_io.build_table(tmp_path, 6000, 4096, bloom_bits=10)
+    file = open(path, "rb").read()
+    d = table_io.dump_blocks(path, str(tmp_path / "d.bin"), True)
+    handles, keys, fh, st = tab.index_host(file, True, internal_keys=True)
+    assert st == tab.LGS_ST_OK and len(handles) == d.n - 2
+    assert fh == table_io.filter_handle(d.contents[-2])
+    assert tab.index_host(file, True, filter_name="filter.other")[2] is None
+
+
+def test_table_index_damaged_files(tab, ref_tables):
+    path, file, d = ref_tables[256]
+    ndata = d.n - 2
+    corrupt = tab.LGS_ST_CORRUPT
+    assert tab.index_host(file[:47])[3] == corrupt                      # table.c:127-128
+    assert tab.index_host(b"")[3] == corrupt
+    assert tab.index_host(file[:-1] + bytes([file[-1] ^ 1]))[3] == corrupt   # magic
+    # An index handle past the end: the read's I/O status (format.c:195-198).
+    io_, is_ = d.index
+    bad = bytearray(file)
+    footer = bytearray(file[-48:])
+    mo, ms = d.metaindex
+    def v(x):
+        out = bytearray()
+        while x >= 128:
+            out.append((x & 127) | 128)
+            x >>= 7
+        out.append(x)
+        return out
+    enc = v(mo) + v(ms) + v(len(file) + 100) + v(is_)
+    footer[:len(enc)] = enc
+    bad[-48:] = footer
+    assert tab.index_host(bytes(bad))[3] == tab.LGS_ST_IOERR
+    # A flipped byte inside the index block: its checksum, when verified.
+    flip = bytearray(file)
+    flip[io_ + 3] ^= 0x40
+    handles, _, _, st = tab.index_host(bytes(flip), paranoid_checks=True)
+    assert st == tab.LGS_ST_BADCRC and handles == []
+    # A cap too small is an error, not a truncated answer.
+    with pytest.raises(Exception):
+        tab.index_host(file, cap=ndata - 1)
+
+
 def test_write_then_read_device_c2_scale(tab):
     """Size-independent property at BASELINE scale: frame 65 536 fillseq blocks
     on the device, read them back (checksums verified): identity."""
