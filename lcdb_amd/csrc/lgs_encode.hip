@@ -455,41 +455,43 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
       e_L = e_C = e_longlen = 0;
     }
 
-    bool done;
+    // The match path computes the copy's end; both paths then update the
+    // loop state with selects (one set of loop-carried values, no per-path
+    // copies of them at the latch).
+    uint32_t at_n = at;
     if (mm) {
       const uint32_t src = 63 - (ncommit - 1);
-      at = lane_val(p, src);
+      const uint32_t base = lane_val(p, src);
       const uint32_t ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
                                                  : lane_val(ct, src);
       // ---- the copy (snappy.c:158-169)
-      const uint32_t base = at;
       uint32_t r = ref + 4;
-      at += 4;
+      at_n = base + 4;
 #pragma clang loop unroll(disable)
       for (;;) {                                                  // snappy.c:163-164
-        const uint32_t q = at + lane;
+        const uint32_t q = at_n + lane;
         // Clamped unconditional reads (q < n implies r + lane < n).
         const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
         const bool same = (q < n) & (x[ra] == x[qa]);
         const uint64_t diff = ballot(!same);
         if (diff) {
-          at += (uint32_t)__builtin_ctzll(diff);
+          at_n += (uint32_t)__builtin_ctzll(diff);
           break;
         }
-        at += kWave;
+        at_n += kWave;
         r += kWave;
       }
 
       // snappy.c:156 + 166: the literal before the copy (empty after a
       // re-match), then the copy -- emitted during the next batch (copies
       // of 68+ bytes, rare, get their tags from emit_copy).
-      const uint32_t clen = at - base, dist = base - ref;
+      const uint32_t clen = at_n - base, dist = base - ref;
       if (DEFER) {
         write_lane2(recA, (base << 16) | clen, recB, dist, nops);
         if (++nops == kWave) {                                    // every 64 ops
           op = flush_ops(o, op, x, recA, recB, kWave, lit0);
           nops = 0;
-          lit0 = at;
+          lit0 = at_n;
         }
       } else {
         const bool longc = clen >= 68;
@@ -499,16 +501,15 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
         e_C = longc ? 0u : clen;
         e_longlen = longc ? clen : 0u;
       }
-      lit = at;
-      done = at >= last;                                          // snappy.c:169
-      start = at + 1;                                             // snappy.c:184-185
-      kv = 0;
-    } else {
-      // No match in this batch: the search ends if a probe before the cut
-      // was past the limit, else continues after the cut.
-      done = (uint32_t)__builtin_popcountll(vmask) < ncut;
-      kv += ncut;
     }
+    // Match: the search restarts after the copy (snappy.c:169, 184-185).
+    // No match: it ends if a probe before the cut was past the limit, else
+    // continues after the cut.
+    const bool done = mm ? at_n >= last : (uint32_t)__builtin_popcountll(vmask) < ncut;
+    lit = mm ? at_n : lit;
+    start = mm ? at_n + 1 : start;
+    kv = mm ? 0u : kv + ncut;
+    at = at_n;
     if (done) break;
   }
   if (DEFER) {
