@@ -736,6 +736,12 @@ static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
 // output from memory, issued when the tag is parsed and used a trip later.
 // A trip = one piece (<= 64 bytes) of one op per lane; every memory
 // operation issued in a trip is waited for once, at the top of the next.
+// TWO (the default): a trip has a second op slot after the flush -- the
+// piece of the op just parsed, if its bytes are in LDS, and the tag after
+// it -- so a literal and a near copy take one trip instead of two.  The
+// ring bounds still hold: the flush leaves < 128 unflushed bytes, each slot
+// adds <= 64, and the next trip's first piece starts below 192.  A far copy
+// met in the second slot is taken only when its source is flushed already.
 // ---------------------------------------------------------------------------
 namespace ring {
 constexpr uint32_t kInRing = 128, kInStride = 208;     // ring + 64 mirror + 16 sink
@@ -763,6 +769,7 @@ struct RingJob {   // 32 bytes
   uint32_t lane, off, cnt, plo, phi, pad0, pad1, pad2;
 };
 
+template <bool TWO>
 __global__ __launch_bounds__(64) void decode_ring_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -816,13 +823,9 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   const uint32_t sink = lane * kInStride + kInSink;   // own slack: no shared-address writes
   uint32_t ra0 = sink, rm0 = sink, ra1 = sink, rm1 = sink;
 
-  for (;;) {
-    const bool active = st == 1 && !(orem == 0 && pos >= slen && F >= made);
-    if (ballot(active) == 0) break;
-
-    // ---- one piece of the current op (snappy.c:210-331) for every lane
-    // whose bytes are in LDS (literal from the window, copy from the ring);
-    // this runs before the wait, so last trip's loads land meanwhile.
+  // One piece (<= 64 bytes) of the current op (snappy.c:210-331) for every
+  // lane whose bytes are in LDS (literal from the window, copy from the ring).
+  auto piece = [&]() {
     if (st == 1 && orem > 0 && !ofar) {
       const bool lit = okind == 0;
       const uint32_t piece = orem < 64 ? orem : 64;
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
             const u32x4 c0 = lrd16(ob + ((made - dist) & (kOutRing - 1)));
             uint32_t w[4] = {0, 0, 0, 0};
             uint32_t r = 0;
-#pragma clang loop unroll(disable)
+  #pragma clang loop unroll(disable)
             for (uint32_t j = 0; j < 16; ++j) {
               w[j >> 2] |= byte_of(c0, r) << (8 * (j & 3u));
               r = r + 1 == dist ? 0 : r + 1;
@@ -852,7 +855,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           }
           out_put(ob, made, p0);
           order();
-#pragma clang loop unroll(disable)
+  #pragma clang loop unroll(disable)
           for (uint32_t k = 1; 16 * k < piece; ++k) {
             const u32x4 v = lrd16(ob + ((made + 16 * k - qq) & (kOutRing - 1)));
             out_put(ob, made + 16 * k, v);
@@ -889,6 +892,47 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
         if (lit) olp += piece;
       }
     }
+  };
+
+  // Parse the next tag (its bytes are in the window); a far copy's bytes are
+  // loaded from the flushed output for the next trip.
+  auto parse = [&](bool second) {
+    if (st == 1 && orem == 0 && pos < slen) {
+      const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
+      if (in_have >= need_to) {
+        const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
+        const bool far = t.kind != 0 && t.dist > kNear;
+        if (t.bad) {
+          st = 0;
+        } else if (!second || !far || made - F + t.len <= t.dist) {
+          // (A far copy parsed in the second slot must find its source
+          // flushed already; otherwise it waits for the next trip's first.)
+          orem = t.len;
+          okind = t.kind == 0 ? 0u : 1u;
+          odist = t.dist;
+          olp = pos + t.hl;
+          pos = t.next;
+          ofar = okind != 0 && odist > kNear;
+          if (ofar) {
+            // Flushed already: it ends <= made - kNear + 64 < F.
+            const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
+            fa0 = ld16(sp);
+            if (orem > 16) fa1 = ld16(sp + 16);
+            if (orem > 32) fa2 = ld16(sp + 32);
+            if (orem > 48) fa3 = ld16(sp + 48);
+          }
+        }
+      }
+    }
+  };
+
+  for (;;) {
+    const bool active = st == 1 && !(orem == 0 && pos >= slen && F >= made);
+    if (ballot(active) == 0) break;
+
+    // ---- one piece of the current op for every lane whose bytes are in LDS;
+    // this runs before the wait, so last trip's loads land meanwhile.
+    piece();
     order();
 
     // ---- everything issued last trip has landed: far-copy pieces (never
@@ -945,30 +989,14 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       if (need) F += fcnt;
     }
 
-    // ---- parse the next tag (its bytes are in the window)
-    if (st == 1 && orem == 0 && pos < slen) {
-      const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
-      if (in_have >= need_to) {
-        const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
-        if (t.bad) {
-          st = 0;
-        } else {
-          orem = t.len;
-          okind = t.kind == 0 ? 0u : 1u;
-          odist = t.dist;
-          olp = pos + t.hl;
-          pos = t.next;
-          ofar = okind != 0 && odist > kNear;
-          if (ofar) {
-            // Flushed already: it ends <= made - kNear + 64 < F.
-            const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
-            fa0 = ld16(sp);
-            if (orem > 16) fa1 = ld16(sp + 16);
-            if (orem > 32) fa2 = ld16(sp + 32);
-            if (orem > 48) fa3 = ld16(sp + 48);
-          }
-        }
-      }
+    // ---- parse the next tag.  TWO: then a second op slot -- its piece, if
+    // its bytes are in LDS, and the tag after it.
+    parse(false);
+    if (TWO) {
+      order();
+      piece();
+      order();
+      parse(true);
     }
 
     // ---- refill requests: the next 64 input bytes, once the 64 they
@@ -1018,8 +1046,14 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
 
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
   const uint32_t grid = (a.n + 63) / 64;
-  hipLaunchKernelGGL(decode_ring_kernel, dim3(grid), dim3(64), 0, s, a.in, a.in_off, a.in_len,
-                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+  // Two op slots per trip; LGS_DECODE_KERNEL=ring1 keeps one (A/B).
+  const char* v = getenv("LGS_DECODE_KERNEL");
+  if (v && !strcmp(v, "ring1"))
+    hipLaunchKernelGGL(decode_ring_kernel<false>, dim3(grid), dim3(64), 0, s, a.in, a.in_off,
+                       a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+  else
+    hipLaunchKernelGGL(decode_ring_kernel<true>, dim3(grid), dim3(64), 0, s, a.in, a.in_off,
+                       a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
   return hipGetLastError();
 }
 
@@ -1043,7 +1077,7 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const char* force = getenv("LGS_DECODE_KERNEL");   // "ring" | "wave" | "lane64" | ...
   if (force) {
-    if (!strcmp(force, "ring")) return launch_decode_ring(a, s);
+    if (!strcmp(force, "ring") || !strcmp(force, "ring1")) return launch_decode_ring(a, s);
     if (!strcmp(force, "lane64")) return launch_decode_lane<64>(a, s);
     if (!strcmp(force, "lane32")) return launch_decode_lane<32>(a, s);
     if (!strcmp(force, "lane16")) return launch_decode_lane<16>(a, s);
