@@ -353,42 +353,37 @@ struct Tag {
 
 __device__ __forceinline__ Tag parse_tag(u32x4 tv, uint32_t pos, uint32_t slen, uint32_t want,
                                          uint32_t made) {
+  // Every field is computed for both kinds and selected: lanes of a wave
+  // parse literals and copies together, so branches would run both sides
+  // anyway and add the exec-mask bookkeeping.
   Tag t;
   const uint32_t tag = tv.x & 0xffu;
-  t.kind = tag & 3u;
+  const uint32_t kind = tag & 3u;
   const uint32_t left = slen - pos;
   const uint32_t b1 = (tv.x >> 8) | (tv.y << 24);              // bytes 1..4
-  t.dist = 0;
-  if (t.kind == 0) {                                            // literal, snappy.c:210-273
-    uint32_t m = tag >> 2;
-    t.hl = 1;
-    t.bad = false;
-    if (m >= 60) {
-      const uint32_t extra = m - 59;
-      t.bad = left - 1 < extra;
-      m = extra == 4 ? b1 : (b1 & ((1u << (8 * extra)) - 1u));
-      t.hl += extra;
-    }
-    t.len = m + 1;
-    t.bad = t.bad || m >= 0x7fffffffu || t.len > want - made || t.len > left - t.hl;
-  } else {                                                      // snappy.c:276-324
-    if (t.kind == 1) {
-      t.len = 4 + ((tag >> 2) & 7u);
-      t.dist = ((tag & 0xe0u) << 3) | (b1 & 0xffu);
-      t.hl = 2;
-    } else if (t.kind == 2) {
-      t.len = 1 + (tag >> 2);
-      t.dist = b1 & 0xffffu;
-      t.hl = 3;
-    } else {
-      t.len = 1 + (tag >> 2);
-      t.dist = b1;
-      t.hl = 5;
-    }
-    t.bad = left < t.hl || t.dist == 0 || t.dist >= 0x80000000u || made < t.dist ||
-            t.len > want - made;
-  }
-  t.next = pos + t.hl + (t.kind == 0 ? t.len : 0);
+  // literal, snappy.c:210-273
+  const uint32_t m0 = tag >> 2;
+  const bool ext = m0 >= 60;
+  const uint32_t extra = ext ? m0 - 59 : 0u;                    // 1..4 length bytes
+  const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
+  const uint32_t m = ext ? (b1 & emask) : m0;
+  const uint32_t lhl = 1 + extra, llen = m + 1;
+  const bool lbad = (ext && left - 1 < extra) || m >= 0x7fffffffu || llen > want - made ||
+                    llen > left - lhl;
+  // copies, snappy.c:276-324
+  const uint32_t clen = kind == 1 ? 4 + ((tag >> 2) & 7u) : 1 + (tag >> 2);
+  const uint32_t cdist = kind == 1 ? ((tag & 0xe0u) << 3) | (b1 & 0xffu)
+                                   : (kind == 2 ? b1 & 0xffffu : b1);
+  const uint32_t chl = kind == 1 ? 2u : (kind == 2 ? 3u : 5u);
+  const bool cbad = left < chl || cdist == 0 || cdist >= 0x80000000u || made < cdist ||
+                    clen > want - made;
+  const bool lit = kind == 0;
+  t.kind = kind;
+  t.len = lit ? llen : clen;
+  t.hl = lit ? lhl : chl;
+  t.dist = lit ? 0u : cdist;
+  t.bad = lit ? lbad : cbad;
+  t.next = pos + t.hl + (lit ? t.len : 0u);
   return t;
 }
 
@@ -862,20 +857,11 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
             order();
           }
         } else {
-          u32x4 c0, c1, c2, c3;
-          if (lit) {
-            const uint8_t* sp = ib + (olp & (kInRing - 1));
-            c0 = lrd16(sp);
-            c1 = lrd16(sp + 16);
-            c2 = lrd16(sp + 32);
-            c3 = lrd16(sp + 48);
-          } else {
-            const uint8_t* sp = ob + ((made - dist) & (kOutRing - 1));
-            c0 = lrd16(sp);
-            c1 = lrd16(sp + 16);
-            c2 = lrd16(sp + 32);
-            c3 = lrd16(sp + 48);
-          }
+          // A literal reads the input window, a copy the output ring.
+          const uint8_t* sp = lit ? ib + (olp & (kInRing - 1))
+                                  : ob + ((made - dist) & (kOutRing - 1));
+          const u32x4 c0 = lrd16(sp), c1 = lrd16(sp + 16), c2 = lrd16(sp + 32),
+                      c3 = lrd16(sp + 48);
           // Period 1/2/4/8: the dist bytes before d as a 16-byte pattern.
           const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
           const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
