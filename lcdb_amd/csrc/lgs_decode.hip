@@ -764,7 +764,7 @@ struct RingJob {   // 32 bytes
   uint32_t lane, off, cnt, plo, phi, pad0, pad1, pad2;
 };
 
-template <bool TWO>
+template <bool TWO, uint32_t BL>
 __global__ __launch_bounds__(64) void decode_ring_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -772,22 +772,24 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
     const uint32_t* __restrict__ index, uint32_t n) {
   using namespace ring;
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[64 * kInStride];
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * kOutStride];
+  // BL lanes decode (BL blocks per wave); with BL < 64 the others only help
+  // with refills and flushes, and each has a 16-byte sink after the rings.
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[BL * kInStride + (64 - BL) * 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[BL * kOutStride];
   __shared__ __attribute__((aligned(16))) RingJob s_job[64];
 
   // Every lane stays to the end: lanes without a block still work for the
   // cooperative refills and flushes.
   const uint32_t lane = threadIdx.x;
-  const uint32_t slot = blockIdx.x * 64 + lane;
-  const bool exists = slot < n;
+  const uint32_t slot = blockIdx.x * BL + lane;
+  const bool exists = lane < BL && slot < n;
   const uint32_t i = exists ? (index ? index[slot] : slot) : 0;
   const gptr<const uint8_t> src = to_global(in) + (exists ? in_off[i] : 0);
   const uint32_t slen = exists ? in_len[i] : 0;
   const gptr<uint8_t> dst = to_global(out) + (exists ? out_off[i] : 0);
   const uint32_t cap = exists ? out_cap[i] : 0;
-  uint8_t* const ib = s_in + lane * kInStride;
-  uint8_t* const ob = s_out + lane * kOutStride + 16;
+  uint8_t* const ib = s_in + (lane < BL ? lane : 0) * kInStride;     // (helpers: unused)
+  uint8_t* const ob = s_out + (lane < BL ? lane : 0) * kOutStride + 16;
 
   // varint32 header, coding.h:169-204.  st: 1 decoding/ok, 0 corrupt,
   // 2 no space, 3 no block.
@@ -815,7 +817,8 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   bool ofar = false;
   u32x4 fa0 = {0, 0, 0, 0}, fa1 = fa0, fa2 = fa0, fa3 = fa0;   // far-copy bytes
   u32x4 rv0 = fa0, rv1 = fa0;                                  // refill bytes (worker)
-  const uint32_t sink = lane * kInStride + kInSink;   // own slack: no shared-address writes
+  const uint32_t sink = lane < BL ? lane * kInStride + kInSink       // own slack: no
+                                  : BL * kInStride + (lane - BL) * 16;  // shared-address writes
   uint32_t ra0 = sink, rm0 = sink, ra1 = sink, rm1 = sink;
 
   // One piece (<= 64 bytes) of the current op (snappy.c:210-331) for every
@@ -1031,15 +1034,23 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
 }
 
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
-  const uint32_t grid = (a.n + 63) / 64;
-  // Two op slots per trip; LGS_DECODE_KERNEL=ring1 keeps one (A/B).
+  // Default: two op slots per trip, 32 blocks per wave (rings for 32 lanes,
+  // 20 KB of LDS: eight waves fit a CU, two per SIMD, and each hides the
+  // other's memory waits).  LGS_DECODE_KERNEL=ring64: 64 blocks per wave
+  // (one per SIMD); ring1: that with one op slot (A/B).
   const char* v = getenv("LGS_DECODE_KERNEL");
   if (v && !strcmp(v, "ring1"))
-    hipLaunchKernelGGL(decode_ring_kernel<false>, dim3(grid), dim3(64), 0, s, a.in, a.in_off,
-                       a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+    hipLaunchKernelGGL((decode_ring_kernel<false, 64>), dim3((a.n + 63) / 64), dim3(64), 0, s,
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
+                       a.status, a.index, a.n);
+  else if (v && !strcmp(v, "ring64"))
+    hipLaunchKernelGGL((decode_ring_kernel<true, 64>), dim3((a.n + 63) / 64), dim3(64), 0, s,
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
+                       a.status, a.index, a.n);
   else
-    hipLaunchKernelGGL(decode_ring_kernel<true>, dim3(grid), dim3(64), 0, s, a.in, a.in_off,
-                       a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+    hipLaunchKernelGGL((decode_ring_kernel<true, 32>), dim3((a.n + 31) / 32), dim3(64), 0, s,
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
+                       a.status, a.index, a.n);
   return hipGetLastError();
 }
 
@@ -1063,7 +1074,7 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const char* force = getenv("LGS_DECODE_KERNEL");   // "ring" | "wave" | "lane64" | ...
   if (force) {
-    if (!strcmp(force, "ring") || !strcmp(force, "ring1")) return launch_decode_ring(a, s);
+    if (!strncmp(force, "ring", 4)) return launch_decode_ring(a, s);
     if (!strcmp(force, "lane64")) return launch_decode_lane<64>(a, s);
     if (!strcmp(force, "lane32")) return launch_decode_lane<32>(a, s);
     if (!strcmp(force, "lane16")) return launch_decode_lane<16>(a, s);

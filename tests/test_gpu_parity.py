@@ -197,7 +197,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lane64", "lane32", "ring", "ring1"])
+@pytest.mark.parametrize("kernel", ["wave", "lane64", "lane32", "ring", "ring1", "ring64"])
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, monkeypatch):
     # Every decode kernel (forced through LGS_DECODE_KERNEL) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -224,7 +224,7 @@ def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
-    for kernel in ("ring", "ring1", "lane64", "lane32", "wave"):
+    for kernel in ("ring", "ring1", "ring64", "lane64", "lane32", "wave"):
         monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
         out = batch.decode_slots(c.len)
         st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
@@ -256,7 +256,7 @@ def test_encode_kernel_variants(gpu, vectors, digests, kernel, monkeypatch):
     assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"]), kernel
 
 
-@pytest.mark.parametrize("kernel", ["ring", "ring1"])
+@pytest.mark.parametrize("kernel", ["ring", "ring1", "ring64"])
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, monkeypatch, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
