@@ -737,6 +737,9 @@ static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
 // ring bounds still hold: the flush leaves < 128 unflushed bytes, each slot
 // adds <= 64, and the next trip's first piece starts below 192.  A far copy
 // met in the second slot is taken only when its source is flushed already.
+// BL: blocks per wave.  With BL = 32 (the default) lanes 32-63 only serve
+// the refill and flush jobs; the rings then fit eight waves in a CU's LDS,
+// two per SIMD, which overlap each other's once-per-trip memory waits.
 // ---------------------------------------------------------------------------
 namespace ring {
 constexpr uint32_t kInRing = 128, kInStride = 208;     // ring + 64 mirror + 16 sink
