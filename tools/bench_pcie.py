@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from lcdb_amd import batch, corpus  # noqa: E402
+from lcdb_amd import batch, corpus, table  # noqa: E402
 
 
 def main() -> None:
@@ -68,13 +68,45 @@ def main() -> None:
 
     te, td, th = timed(enc_pass), timed(dec_pass), timed(h2d_raw)
     assert bool((st == 1).all())
+
+    # The table paths as lcdb would call them: the
+    # data-block region of a table written from host blocks (H2D raw, encode,
+    # 12.5 % rule, trailers, packing, D2H of exactly the region), and that
+    # region read back (H2D region, checksums, decode, D2H blocks).
+    max_len, raw_total = int(c.len.max()), int(c.len.sum())
+    d_file, hoff, hsize, end = table.write_blocks(raw.buf, raw.off, raw.len, 1, 0, max_len,
+                                                  raw_total)
+    torch.cuda.synchronize()
+    region = int(end.item())
+    h_file = torch.empty(d_file.numel(), dtype=torch.uint8).pin_memory()
+
+    def tw_pass():
+        raw.buf.copy_(h_raw, non_blocking=True)
+        f, _, _, e = table.write_blocks(raw.buf, raw.off, raw.len, 1, 0, max_len, raw_total)
+        n = int(e.item())                     # the host needs the region's size
+        h_file[:n].copy_(f[:n], non_blocking=True)
+
+    olen = torch.zeros(c.n, dtype=torch.int32, device="cuda")
+
+    def tr_pass():
+        d_file[:region].copy_(h_file[:region], non_blocking=True)
+        table.read_blocks(d_file, region, hoff, hsize, out.buf, out.off, out.cap, out.max_cap,
+                          True, olen, st)
+        h_out.copy_(out.buf, non_blocking=True)
+
+    ttw = timed(tw_pass)
+    ttr = timed(tr_pass)
+    assert bool((st == 1).all()) and torch.equal(olen, raw.len)
     rb = c.raw_bytes
     print(json.dumps({
         "blocks": c.n, "raw_bytes": rb, "comp_bytes_packed": comp_bytes,
         "comp_slot_bytes": comp.buf.numel(), "h2d_raw_GBps": h_raw.numel() / th / 1e9,
         "encode_pcie_GiBps": rb / te / 2**30, "decode_pcie_GiBps": rb / td / 2**30,
         "roundtrip_pcie_GiBps": rb / (te + td) / 2**30,
-        "encode_pass_ms": te * 1e3, "decode_pass_ms": td * 1e3}))
+        "encode_pass_ms": te * 1e3, "decode_pass_ms": td * 1e3,
+        "table_region_bytes": region,
+        "table_write_pcie_GiBps": rb / ttw / 2**30, "table_read_pcie_GiBps": rb / ttr / 2**30,
+        "table_write_pass_ms": ttw * 1e3, "table_read_pass_ms": ttr * 1e3}))
 
 
 if __name__ == "__main__":
