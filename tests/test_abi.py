@@ -67,3 +67,28 @@ def test_host_side_size_functions_match_oracle(vectors):
     for v in vectors:
         s = v.a if v.kind == 1 else v.b
         assert snappy.decode_size(s) == orc.decode_size(s), v.name
+
+
+def test_host_side_bloom_and_filter_block_sizes_match_oracle():
+    """lgs_bloom_filter_size equals the reference filter's length, and
+    lgs_filter_block_bound covers every filter block the oracle builds
+    (pure host functions: no GPU)."""
+    import random
+
+    from lcdb_amd import bloom
+    from test_bloom_oracle import random_table_layout
+    orc = oracle.bloom_restatement()
+    for n in (0, 1, 5, 36, 1000):
+        for bpk in (0, 1, 10, 16, 50):
+            keys = [b"%08d" % k for k in range(n)]
+            want = len(orc.build(keys, bpk)) if n else 0
+            assert bloom.filter_size(n, bpk) == want, (n, bpk)
+    rng = random.Random(9)
+    for _ in range(200):
+        internal = rng.random() < 0.5
+        blocks, off, end = random_table_layout(rng, internal)
+        bpk = rng.choice([0, 1, 10, 16, 44])
+        fb = orc.filter_block(blocks, off, end, bpk, internal)
+        nkeys = sum(len(b) for b in blocks)
+        assert len(fb) <= bloom.filter_block_bound(nkeys, len(blocks), end, bpk)
+        assert bloom.filter_block_scratch(end) > 0
