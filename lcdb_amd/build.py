@@ -54,7 +54,7 @@ def build_hip(force: bool = False, extra: list[str] | None = None) -> str:
     if force or _stale(LIB, deps):
         tmp = LIB + ".tmp"
         _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wextra", *srcs, "-o", tmp, *(extra or [])])
+              "-Wall", "-Wextra", "-pthread", *srcs, "-o", tmp, *(extra or [])])
         os.replace(tmp, LIB)
     return LIB
 

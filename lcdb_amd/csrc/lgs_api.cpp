@@ -19,6 +19,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
 #include "../../include/lcdb_gpu_snappy.h"
 
 #include "lgs_launch.h"
@@ -55,10 +63,92 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) & ~(a - 1); }
 
 size_t bound_of(size_t n) { return 32 + n + n / 6; }   // snappy.c:354
 
+// Host staging copies (pageable caller buffers <-> the pinned arena) split
+// over threads once a call moves more than 8 MB: one thread copies ~10 GB/s,
+// slower than the transfers it feeds.  Threads are per call (no shared pool:
+// callers enter from several threads at once).  LGS_HOST_THREADS overrides
+// the count (default: the hardware threads, at most 16).
+unsigned host_threads(size_t bytes) {
+  static const unsigned hw = [] {
+    const char* e = getenv("LGS_HOST_THREADS");
+    int v = e ? atoi(e) : 0;
+    if (v <= 0) v = (int)std::thread::hardware_concurrency();
+    if (v > 16) v = 16;
+    return v > 0 ? (unsigned)v : 1u;
+  }();
+  return bytes < (8u << 20) ? 1u : hw;
+}
+
+// Worker threads for the staging copies: created once, never destroyed
+// (like the HIP resources below), shared by every calling thread.
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool* p = new Pool(host_threads(~(size_t)0));
+    return *p;
+  }
+  // f(0 .. t-1): part 0 on the caller, the others on workers.
+  void run(unsigned t, const std::function<void(unsigned)>& f) {
+    std::mutex m;
+    std::condition_variable cv;
+    unsigned left = t - 1;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (unsigned k = 1; k < t; ++k)
+        q_.push_back([&, k] {
+          f(k);
+          std::lock_guard<std::mutex> g2(m);      // the caller's stack frame outlives this
+          if (--left == 0) cv.notify_one();
+        });
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return left == 0; });
+  }
+
+ private:
+  explicit Pool(unsigned n) {
+    for (unsigned k = 1; k < n; ++k) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        job = std::move(q_.front());
+        q_.pop_front();
+      }
+      job();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+
+// f(i0, i1) over [0, n) in contiguous ranges, on host_threads(bytes) threads.
+template <class F>
+void par_for(uint32_t n, size_t bytes, const F& f) {
+  const unsigned t = host_threads(bytes);
+  if (t <= 1 || n < 2 * t) {
+    f(0u, n);
+    return;
+  }
+  const uint32_t per = (n + t - 1) / t;
+  Pool::get().run(t, [&](unsigned k) {
+    const uint32_t a = k * per, b = a + per < n ? a + per : n;
+    if (a < b) f(a, b);
+  });
+}
+
 struct Ctx {
   int device = -1;          // device this context's resources live on
   int want_device = -1;     // lgs_set_device() choice (-1: current device)
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;   // the chunk pipeline's second stream (lazily)
+  hipEvent_t done[2] = {nullptr, nullptr};
   uint8_t* d_buf = nullptr;
   size_t d_cap = 0;
   uint8_t* h_buf = nullptr; // pinned
@@ -111,6 +201,68 @@ int ctx_reserve(Ctx& c, size_t dev_bytes, size_t pin_bytes) {
     c.h_cap = cap;
   }
   return LGS_OK;
+}
+
+// Two streams and two events for the chunk pipeline below.
+int ctx_pipeline(Ctx& c) {
+  if (c.stream2 == nullptr) LGS_HIP(hipStreamCreateWithFlags(&c.stream2, hipStreamNonBlocking));
+  for (hipEvent_t& e : c.done)
+    if (e == nullptr) LGS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return LGS_OK;
+}
+
+// Runs `chunks` independent pieces of a host call through two streams:
+// stage(k) fills chunk k's own part of the pinned arena, launch(k, stream)
+// enqueues its uploads, kernels and downloads, finish(k) copies its results
+// out once they have arrived.  Staging chunk k+1 and finishing chunk k-1 on
+// the host overlap chunk k's transfers and kernels, and consecutive chunks'
+// transfers overlap each other's kernels.  Chunks use disjoint parts of the
+// arenas; a stream's scratch is reused only after that stream's previous
+// chunk has finished.
+template <class Stage, class Launch, class Finish>
+int pipeline(Ctx& c, uint32_t chunks, const Stage& stage, const Launch& launch,
+             const Finish& finish) {
+  LGS_TRY(ctx_pipeline(c));
+  const hipStream_t st[2] = {c.stream, c.stream2};
+  for (uint32_t k = 0; k < chunks; ++k) {
+    stage(k);
+    LGS_TRY(launch(k, st[k & 1]));
+    LGS_HIP(hipEventRecord(c.done[k & 1], st[k & 1]));
+    if (k >= 1) {
+      LGS_HIP(hipEventSynchronize(c.done[(k - 1) & 1]));
+      LGS_TRY(finish(k - 1));
+    }
+  }
+  LGS_HIP(hipEventSynchronize(c.done[(chunks - 1) & 1]));
+  return finish(chunks - 1);
+}
+
+// Chunk boundaries: [first[k], first[k+1]) over n items of `bytes` in total,
+// about LGS_HOST_CHUNK_MB (default 32; 0: no chunking) each; one chunk for
+// small calls.
+size_t chunk_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("LGS_HOST_CHUNK_MB");
+    return (size_t)(e ? atoi(e) : 32) << 20;
+  }();
+  return v;
+}
+
+std::vector<uint32_t> chunk_bounds(uint32_t n, size_t bytes, const uint32_t* len) {
+  const size_t kChunkBytes = chunk_bytes();
+  std::vector<uint32_t> first{0};
+  if (kChunkBytes > 0 && bytes >= 2 * kChunkBytes) {
+    size_t acc = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      acc += len[i];
+      if (acc >= kChunkBytes && i + 1 < n) {
+        first.push_back(i + 1);
+        acc = 0;
+      }
+    }
+  }
+  first.push_back(n);
+  return first;
 }
 
 // Offsets into a staging area, 256-byte aligned.  The pinned arena and the
@@ -376,13 +528,15 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   uint64_t* ooff = (uint64_t*)(h + o_ooff);
   size_t ia = o_in, oa = o_out;
   for (uint32_t i = 0; i < n; ++i) {
-    memcpy(h + ia, in + in_off[i], in_len[i]);
     ioff[i] = ia;
     ilen[i] = in_len[i];
     ooff[i] = oa;
     ia += align_up(in_len[i], 16);
     oa += align_up(bound_of(in_len[i]), 16);
   }
+  par_for(n, in_total, [&](uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0; i < i1; ++i) memcpy(h + ioff[i], in + in_off[i], in_len[i]);
+  });
   LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
   EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
                (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen), nullptr, nullptr, n};
@@ -391,10 +545,12 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
                          c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
   const uint32_t* olen = (const uint32_t*)(h + o_olen);
-  for (uint32_t i = 0; i < n; ++i) {
-    memcpy(out + out_off[i], h + ooff[i], olen[i]);
-    out_len[i] = olen[i];
-  }
+  par_for(n, in_total, [&](uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0; i < i1; ++i) {
+      memcpy(out + out_off[i], h + ooff[i], olen[i]);
+      out_len[i] = olen[i];
+    }
+  });
   return LGS_OK;
 }
 
@@ -433,7 +589,6 @@ int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   uint32_t* ocap = (uint32_t*)(h + o_ocap);
   size_t ia = o_in, oa = o_out;
   for (uint32_t i = 0; i < n; ++i) {
-    memcpy(h + ia, in + in_off[i], in_len[i]);
     ioff[i] = ia;
     ilen[i] = in_len[i];
     ooff[i] = oa;
@@ -441,6 +596,9 @@ int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
     ia += align_up(in_len[i], 16);
     oa += align_up(out_cap[i], 16);
   }
+  par_for(n, in_total, [&](uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0; i < i1; ++i) memcpy(h + ioff[i], in + in_off[i], in_len[i]);
+  });
   LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
   DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
                (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
@@ -449,11 +607,13 @@ int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
   const uint32_t* olen = (const uint32_t*)(h + o_olen);
-  for (uint32_t i = 0; i < n; ++i) {
-    status[i] = h[o_st + i];
-    out_len[i] = olen[i];
-    if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
-  }
+  par_for(n, out_total, [&](uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0; i < i1; ++i) {
+      status[i] = h[o_st + i];
+      out_len[i] = olen[i];
+      if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
+    }
+  });
   return LGS_OK;
 }
 
@@ -604,54 +764,107 @@ int lgs_table_write_host(const uint8_t* raw, const uint64_t* raw_off, const uint
     return fail(LGS_EINVAL, "unknown compression type %d", compression);
   Ctx& c = t_ctx;
   LGS_TRY(ctx_ready(c));
-  size_t in_total = 0, file_max = 0;
+  size_t in_total = 0;
   uint32_t max_in = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (raw_len[i] > 0x7fffffffu) return fail(LGS_EINVAL, "block %u too large", i);
     in_total += align_up(raw_len[i], 16);
-    file_max += (size_t)raw_len[i] + LGS_TRAILER_SIZE;
     if (raw_len[i] > max_in) max_in = raw_len[i];
   }
-  const WriteScratch W(n, in_total);
-  Layout L;  // upload | download | device-only
+  // Chunks of consecutive blocks are framed independently at file offset 0
+  // (a block's framing does not depend on where it lands) and placed at
+  // their running offset when they come back.
+  const std::vector<uint32_t> first = chunk_bounds(n, in_total, raw_len);
+  const uint32_t chunks = (uint32_t)first.size() - 1;
+  std::vector<size_t> fo(chunks + 1, 0);   // each chunk's file-region bound in the arena
+  uint32_t max_n = 0;
+  uint64_t max_raw = 0;
+  for (uint32_t k = 0; k < chunks; ++k) {
+    uint64_t r = 0;
+    for (uint32_t i = first[k]; i < first[k + 1]; ++i) r += raw_len[i];
+    fo[k + 1] = fo[k] + align_up((size_t)r + LGS_TRAILER_SIZE * (first[k + 1] - first[k]) + 16, 256);
+    if (first[k + 1] - first[k] > max_n) max_n = first[k + 1] - first[k];
+    if (r > max_raw) max_raw = r;
+  }
+  const WriteScratch W(max_n, max_raw + 16 * (uint64_t)max_n);
+  Layout L;  // uploads | downloads | device-only
   const size_t o_in = L.take(in_total + 16);
   const size_t o_ioff = L.take(8 * (size_t)n);
   const size_t o_ilen = L.take(4 * (size_t)n);
-  const size_t up_end = L.at;
   const size_t o_hoff = L.take(8 * (size_t)n);
   const size_t o_hsize = L.take(8 * (size_t)n);
-  const size_t o_end = L.take(8);
-  const size_t o_file = L.take(file_max + 16);
-  const size_t down_end = L.at;
-  const size_t o_scr = L.take(W.total);
-  LGS_TRY(ctx_reserve(c, L.at, down_end));
+  const size_t o_end = L.take(8 * (size_t)chunks);
+  const size_t o_file = L.take(fo[chunks]);
+  const size_t pin_end = L.at;
+  const size_t o_scr = L.take(2 * align_up(W.total, 256));
+  LGS_TRY(ctx_reserve(c, L.at, pin_end));
   uint8_t* h = c.h_buf;
   uint8_t* d = c.d_buf;
   uint64_t* ioff = (uint64_t*)(h + o_ioff);
   uint32_t* ilen = (uint32_t*)(h + o_ilen);
   size_t ia = o_in;
   for (uint32_t i = 0; i < n; ++i) {
-    memcpy(h + ia, raw + raw_off[i], raw_len[i]);
     ioff[i] = ia;
     ilen[i] = raw_len[i];
     ia += align_up(raw_len[i], 16);
   }
-  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
-  LGS_TRY(table_write(d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), n, max_in,
-                      compression, base, d + o_file, (uint64_t*)(d + o_hoff),
-                      (uint64_t*)(d + o_hsize), (uint64_t*)(d + o_end), d + o_scr, W, c.stream));
-  LGS_HIP(hipMemcpyAsync(h + o_hoff, d + o_hoff, o_file - o_hoff, hipMemcpyDeviceToHost,
-                         c.stream));
-  LGS_HIP(hipStreamSynchronize(c.stream));
-  const uint64_t e = *(const uint64_t*)(h + o_end);
-  const size_t bytes = (size_t)(e - base);
-  if (bytes > file_cap) return fail(LGS_EINVAL, "file buffer of %zu bytes, %zu needed", file_cap, bytes);
-  LGS_HIP(hipMemcpyAsync(h + o_file, d + o_file, bytes, hipMemcpyDeviceToHost, c.stream));
-  LGS_HIP(hipStreamSynchronize(c.stream));
-  memcpy(file, h + o_file, bytes);
-  memcpy(handle_off, h + o_hoff, 8 * (size_t)n);
-  memcpy(handle_size, h + o_hsize, 8 * (size_t)n);
-  *end = e;
+  uint64_t at = base;                      // file offset of the next chunk
+  auto stage = [&](uint32_t k) {
+    par_for(first[k + 1] - first[k], ioff[first[k + 1] - 1] + 16 - ioff[first[k]],
+            [&](uint32_t j0, uint32_t j1) {
+              for (uint32_t i = first[k] + j0; i < first[k] + j1; ++i)
+                memcpy(h + ioff[i], raw + raw_off[i], raw_len[i]);
+            });
+  };
+  auto launch = [&](uint32_t k, hipStream_t s) -> int {
+    const uint32_t i0 = first[k], m = first[k + 1] - i0;
+    const size_t a0 = ioff[i0], a1 = ioff[first[k + 1] - 1] + align_up(raw_len[first[k + 1] - 1], 16);
+    LGS_HIP(hipMemcpyAsync(d + a0, h + a0, a1 - a0, hipMemcpyHostToDevice, s));
+    LGS_HIP(hipMemcpyAsync(d + o_ioff + 8 * (size_t)i0, h + o_ioff + 8 * (size_t)i0, 8 * (size_t)m,
+                           hipMemcpyHostToDevice, s));
+    LGS_HIP(hipMemcpyAsync(d + o_ilen + 4 * (size_t)i0, h + o_ilen + 4 * (size_t)i0, 4 * (size_t)m,
+                           hipMemcpyHostToDevice, s));
+    uint8_t* scr = d + o_scr + (k & 1) * align_up(W.total, 256);
+    LGS_TRY(table_write(d, (const uint64_t*)(d + o_ioff) + i0, (const uint32_t*)(d + o_ilen) + i0,
+                        m, max_in, compression, 0, d + o_file + fo[k],
+                        (uint64_t*)(d + o_hoff) + i0, (uint64_t*)(d + o_hsize) + i0,
+                        (uint64_t*)(d + o_end) + k, scr, W, s));
+    LGS_HIP(hipMemcpyAsync(h + o_hoff + 8 * (size_t)i0, d + o_hoff + 8 * (size_t)i0,
+                           8 * (size_t)m, hipMemcpyDeviceToHost, s));
+    LGS_HIP(hipMemcpyAsync(h + o_hsize + 8 * (size_t)i0, d + o_hsize + 8 * (size_t)i0,
+                           8 * (size_t)m, hipMemcpyDeviceToHost, s));
+    LGS_HIP(hipMemcpyAsync(h + o_end + 8 * (size_t)k, d + o_end + 8 * (size_t)k, 8,
+                           hipMemcpyDeviceToHost, s));
+    // The region's size is known only on the device: its bound comes back.
+    LGS_HIP(hipMemcpyAsync(h + o_file + fo[k], d + o_file + fo[k], fo[k + 1] - fo[k],
+                           hipMemcpyDeviceToHost, s));
+    return LGS_OK;
+  };
+  auto finish = [&](uint32_t k) -> int {
+    const uint32_t i0 = first[k], m = first[k + 1] - i0;
+    const uint64_t bytes = ((const uint64_t*)(h + o_end))[k];
+    if (at - base + bytes > file_cap)
+      return fail(LGS_EINVAL, "file buffer of %zu bytes, %zu needed", file_cap,
+                  (size_t)(at - base + bytes));
+    const uint8_t* src = h + o_file + fo[k];
+    uint8_t* dst = file + (at - base);
+    const uint32_t parts = 64;
+    const size_t per = ((size_t)bytes + parts - 1) / parts;
+    par_for(parts, (size_t)bytes, [&](uint32_t q0, uint32_t q1) {
+      const size_t x0 = (size_t)q0 * per, x1 = (size_t)q1 * per < bytes ? (size_t)q1 * per : bytes;
+      if (x0 < x1) memcpy(dst + x0, src + x0, x1 - x0);
+    });
+    const uint64_t* ho = (const uint64_t*)(h + o_hoff) + i0;
+    const uint64_t* hs = (const uint64_t*)(h + o_hsize) + i0;
+    for (uint32_t j = 0; j < m; ++j) {
+      handle_off[i0 + j] = ho[j] + at;
+      handle_size[i0 + j] = hs[j];
+    }
+    at += bytes;
+    return LGS_OK;
+  };
+  LGS_TRY(pipeline(c, chunks, stage, launch, finish));
+  *end = at;
   return LGS_OK;
 }
 
@@ -702,7 +915,6 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
     const uint64_t o = handle_off[i], sz = handle_size[i];
     hsize[i] = sz;
     if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE) {
-      memcpy(h + o_blk + ba, file + o, (size_t)sz + LGS_TRAILER_SIZE);
       hoff[i] = ba;
       ba += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
     } else {
@@ -712,6 +924,11 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
     ocap[i] = out_cap[i];
     oa += align_up(out_cap[i], 16);
   }
+  par_for(n, blk_total, [&](uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0; i < i1; ++i)
+      if (hoff[i] <= img_len)
+        memcpy(h + o_blk + hoff[i], file + handle_off[i], (size_t)hsize[i] + LGS_TRAILER_SIZE);
+  });
   LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
   LGS_TRY(table_read(d + o_blk, img_len, (const uint64_t*)(d + o_hoff),
                      (const uint64_t*)(d + o_hsize), n, verify_checksums, d,
@@ -720,11 +937,13 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
   LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
   const uint32_t* olen = (const uint32_t*)(h + o_olen);
-  for (uint32_t i = 0; i < n; ++i) {
-    status[i] = h[o_st + i];
-    out_len[i] = olen[i];
-    if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
-  }
+  par_for(n, out_total, [&](uint32_t i0, uint32_t i1) {
+    for (uint32_t i = i0; i < i1; ++i) {
+      status[i] = h[o_st + i];
+      out_len[i] = olen[i];
+      if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
+    }
+  });
   return LGS_OK;
 }
 

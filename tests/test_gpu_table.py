@@ -268,6 +268,28 @@ def test_table_index_damaged_files(tab, ref_tables):
         tab.index_host(file, cap=ndata - 1)
 
 
+def test_host_paths_chunked_c2_scale(tab):
+    """The host-buffer table paths at BASELINE scale, where they run as a
+    two-stream chunk pipeline: the region equals the device path's byte for
+    byte, and reading it back through the host path returns every block."""
+    import torch
+    from lcdb_amd import batch, corpus
+    c = corpus.fillseq(65536)
+    blocks = c.blocks()
+    region, hoff, hsize, end = tab.write_blocks_host(blocks, tab.LGS_SNAPPY_COMPRESSION, 7)
+    raw = batch.upload(c)
+    d_file, dho, dhs, dend = tab.write_blocks(raw.buf, raw.off, raw.len, 1, 7)
+    torch.cuda.synchronize()
+    assert end == int(dend.cpu()[0])
+    assert region == d_file[:end - 7].cpu().numpy().tobytes()
+    assert np.array_equal(hoff, dho.cpu().numpy().astype(np.uint64))
+    assert np.array_equal(hsize, dhs.cpu().numpy().astype(np.uint64))
+    image = b"\0" * 7 + region
+    res, st = tab.read_blocks_host(image, hoff, hsize, [int(x) for x in c.len])
+    assert all(int(x) == tab.LGS_ST_OK for x in st)
+    assert res == blocks
+
+
 def test_write_then_read_device_c2_scale(tab):
     """Size-independent property at BASELINE scale: frame 65 536 fillseq blocks
     on the device, read them back (checksums verified): identity."""
