@@ -238,12 +238,12 @@ int pipeline(Ctx& c, uint32_t chunks, const Stage& stage, const Launch& launch,
 }
 
 // Chunk boundaries: [first[k], first[k+1]) over n items of `bytes` in total,
-// about LGS_HOST_CHUNK_MB (default 32; 0: no chunking) each; one chunk for
+// about LGS_HOST_CHUNK_MB (default 64; 0: no chunking) each; one chunk for
 // small calls.
 size_t chunk_bytes() {
   static const size_t v = [] {
     const char* e = getenv("LGS_HOST_CHUNK_MB");
-    return (size_t)(e ? atoi(e) : 32) << 20;
+    return (size_t)(e ? atoi(e) : 64) << 20;
   }();
   return v;
 }
@@ -889,61 +889,94 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
     out_total += align_up(out_cap[i], 16);
     if (out_cap[i] > max_cap) max_cap = out_cap[i];
   }
-  const ReadScratch R(n);
+  // Chunks of consecutive handles go through the two-stream pipeline (see
+  // pipeline()); each chunk's packed ranges are contiguous in the image.
+  const std::vector<uint32_t> first = chunk_bounds(n, out_total, out_cap);
+  const uint32_t chunks = (uint32_t)first.size() - 1;
+  uint32_t max_n = 0;
+  for (uint32_t k = 0; k < chunks; ++k)
+    if (first[k + 1] - first[k] > max_n) max_n = first[k + 1] - first[k];
+  const ReadScratch R(max_n);
   Layout L;
   const size_t o_blk = L.take(blk_total + 16);
   const size_t o_hoff = L.take(8 * (size_t)n);
   const size_t o_hsize = L.take(8 * (size_t)n);
   const size_t o_ooff = L.take(8 * (size_t)n);
   const size_t o_ocap = L.take(4 * (size_t)n);
-  const size_t up_end = L.at;
   const size_t o_st = L.take((size_t)n);
   const size_t o_olen = L.take(4 * (size_t)n);
   const size_t o_out = L.take(out_total + 16);
-  const size_t down_end = L.at;
-  const size_t o_scr = L.take(R.total);
-  LGS_TRY(ctx_reserve(c, L.at, down_end));
+  const size_t pin_end = L.at;
+  const size_t o_scr = L.take(2 * align_up(R.total, 256));
+  LGS_TRY(ctx_reserve(c, L.at, pin_end));
   uint8_t* h = c.h_buf;
   uint8_t* d = c.d_buf;
   uint64_t* hoff = (uint64_t*)(h + o_hoff);
   uint64_t* hsize = (uint64_t*)(h + o_hsize);
   uint64_t* ooff = (uint64_t*)(h + o_ooff);
   uint32_t* ocap = (uint32_t*)(h + o_ocap);
+  std::vector<size_t> pa(chunks + 1, 0);     // each chunk's packed range in the image
   size_t ba = 0, oa = o_out;
   const uint64_t img_len = blk_total + 16;   // device file image: the packed ranges
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t o = handle_off[i], sz = handle_size[i];
-    hsize[i] = sz;
-    if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE) {
-      hoff[i] = ba;
-      ba += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
-    } else {
-      hoff[i] = img_len + 1;
+  for (uint32_t k = 0; k < chunks; ++k) {
+    pa[k] = ba;
+    for (uint32_t i = first[k]; i < first[k + 1]; ++i) {
+      const uint64_t o = handle_off[i], sz = handle_size[i];
+      hsize[i] = sz;
+      if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE) {
+        hoff[i] = ba;
+        ba += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
+      } else {
+        hoff[i] = img_len + 1;
+      }
+      ooff[i] = oa;
+      ocap[i] = out_cap[i];
+      oa += align_up(out_cap[i], 16);
     }
-    ooff[i] = oa;
-    ocap[i] = out_cap[i];
-    oa += align_up(out_cap[i], 16);
   }
-  par_for(n, blk_total, [&](uint32_t i0, uint32_t i1) {
-    for (uint32_t i = i0; i < i1; ++i)
-      if (hoff[i] <= img_len)
-        memcpy(h + o_blk + hoff[i], file + handle_off[i], (size_t)hsize[i] + LGS_TRAILER_SIZE);
-  });
-  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
-  LGS_TRY(table_read(d + o_blk, img_len, (const uint64_t*)(d + o_hoff),
-                     (const uint64_t*)(d + o_hsize), n, verify_checksums, d,
-                     (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap), max_cap,
-                     (uint32_t*)(d + o_olen), d + o_st, d + o_scr, R, c.stream));
-  LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
-  LGS_HIP(hipStreamSynchronize(c.stream));
-  const uint32_t* olen = (const uint32_t*)(h + o_olen);
-  par_for(n, out_total, [&](uint32_t i0, uint32_t i1) {
-    for (uint32_t i = i0; i < i1; ++i) {
-      status[i] = h[o_st + i];
-      out_len[i] = olen[i];
-      if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
-    }
-  });
+  pa[chunks] = ba;
+  auto stage = [&](uint32_t k) {
+    par_for(first[k + 1] - first[k], pa[k + 1] - pa[k], [&](uint32_t j0, uint32_t j1) {
+      for (uint32_t i = first[k] + j0; i < first[k] + j1; ++i)
+        if (hoff[i] <= img_len)
+          memcpy(h + o_blk + hoff[i], file + handle_off[i], (size_t)hsize[i] + LGS_TRAILER_SIZE);
+    });
+  };
+  auto launch = [&](uint32_t k, hipStream_t s) -> int {
+    const uint32_t i0 = first[k], m = first[k + 1] - i0, il = first[k + 1] - 1;
+    if (pa[k + 1] > pa[k])
+      LGS_HIP(hipMemcpyAsync(d + o_blk + pa[k], h + o_blk + pa[k], pa[k + 1] - pa[k],
+                             hipMemcpyHostToDevice, s));
+    for (const size_t o : {o_hoff, o_hsize, o_ooff})
+      LGS_HIP(hipMemcpyAsync(d + o + 8 * (size_t)i0, h + o + 8 * (size_t)i0, 8 * (size_t)m,
+                             hipMemcpyHostToDevice, s));
+    LGS_HIP(hipMemcpyAsync(d + o_ocap + 4 * (size_t)i0, h + o_ocap + 4 * (size_t)i0,
+                           4 * (size_t)m, hipMemcpyHostToDevice, s));
+    uint8_t* scr = d + o_scr + (k & 1) * align_up(R.total, 256);
+    LGS_TRY(table_read(d + o_blk, img_len, (const uint64_t*)(d + o_hoff) + i0,
+                       (const uint64_t*)(d + o_hsize) + i0, m, verify_checksums, d,
+                       (const uint64_t*)(d + o_ooff) + i0, (const uint32_t*)(d + o_ocap) + i0,
+                       max_cap, (uint32_t*)(d + o_olen) + i0, d + o_st + i0, scr, R, s));
+    LGS_HIP(hipMemcpyAsync(h + o_st + i0, d + o_st + i0, m, hipMemcpyDeviceToHost, s));
+    LGS_HIP(hipMemcpyAsync(h + o_olen + 4 * (size_t)i0, d + o_olen + 4 * (size_t)i0,
+                           4 * (size_t)m, hipMemcpyDeviceToHost, s));
+    const size_t oe = ooff[il] + align_up(out_cap[il], 16);
+    LGS_HIP(hipMemcpyAsync(h + ooff[i0], d + ooff[i0], oe - ooff[i0], hipMemcpyDeviceToHost, s));
+    return LGS_OK;
+  };
+  auto finish = [&](uint32_t k) -> int {
+    const uint32_t* olen = (const uint32_t*)(h + o_olen);
+    const size_t bytes = ooff[first[k + 1] - 1] + out_cap[first[k + 1] - 1] - ooff[first[k]];
+    par_for(first[k + 1] - first[k], bytes, [&](uint32_t j0, uint32_t j1) {
+      for (uint32_t i = first[k] + j0; i < first[k] + j1; ++i) {
+        status[i] = h[o_st + i];
+        out_len[i] = olen[i];
+        if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
+      }
+    });
+    return LGS_OK;
+  };
+  LGS_TRY(pipeline(c, chunks, stage, launch, finish));
   return LGS_OK;
 }
 
