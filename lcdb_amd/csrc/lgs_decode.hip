@@ -763,8 +763,16 @@ __device__ __forceinline__ void out_put(uint8_t* ob, uint32_t p, u32x4 v) {
   lwr16(ob + r2, v);
 }
 
-struct RingJob {   // 32 bytes
-  uint32_t lane, off, cnt, plo, phi, pad0, pad1, pad2;
+// A cooperative job (a refill or a flush) of one lane, 16 bytes: the lane
+// rides in the top byte of the pointer's high word (virtual addresses are
+// 48-bit).
+struct RingJob {
+  uint32_t off, cnt, plo, phil;
+  __device__ RingJob() = default;
+  __device__ RingJob(uint32_t ln, uint32_t o, uint32_t c, uint64_t p)
+      : off(o), cnt(c), plo((uint32_t)p), phil((uint32_t)(p >> 32) | (ln << 24)) {}
+  __device__ uint32_t lane() const { return phil >> 24; }
+  __device__ uint64_t ptr() const { return ((uint64_t)(phil & 0xffffffu) << 32) | plo; }
 };
 
 template <bool TWO, uint32_t BL>
@@ -776,10 +784,12 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     const uint32_t* __restrict__ index, uint32_t n) {
   using namespace ring;
   // BL lanes decode (BL blocks per wave); with BL < 64 the others only help
-  // with refills and flushes, and each has a 16-byte sink after the rings.
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[BL * kInStride + (64 - BL) * 16];
+  // with refills and flushes.  At most BL lanes post a flush job and at most
+  // min(BL, 32) a refill job per trip.
+  constexpr uint32_t kJobs = BL > 32 ? BL : 32;
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[BL * kInStride];
   __shared__ __attribute__((aligned(16))) uint8_t s_out[BL * kOutStride];
-  __shared__ __attribute__((aligned(16))) RingJob s_job[64];
+  __shared__ __attribute__((aligned(16))) RingJob s_job[kJobs];
 
   // Every lane stays to the end: lanes without a block still work for the
   // cooperative refills and flushes.
@@ -820,8 +830,9 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   bool ofar = false;
   u32x4 fa0 = {0, 0, 0, 0}, fa1 = fa0, fa2 = fa0, fa3 = fa0;   // far-copy bytes
   u32x4 rv0 = fa0, rv1 = fa0;                                  // refill bytes (worker)
-  const uint32_t sink = lane < BL ? lane * kInStride + kInSink       // own slack: no
-                                  : BL * kInStride + (lane - BL) * 16;  // shared-address writes
+  // A lane's sink for dropped refill writes: its own slack (helpers share a
+  // decoding lane's).
+  const uint32_t sink = (lane < BL ? lane : (lane - BL) % BL) * kInStride + kInSink;
   uint32_t ra0 = sink, rm0 = sink, ra1 = sink, rm1 = sink;
 
   // One piece (<= 64 bytes) of the current op (snappy.c:210-331) for every
@@ -959,7 +970,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       const uint32_t total = uni((uint32_t)__builtin_popcountll(m));
       if (need) {
         const uint64_t dp = reinterpret_cast<uint64_t>(dst);
-        s_job[j] = RingJob{lane, F, fcnt, (uint32_t)dp, (uint32_t)(dp >> 32), 0, 0, 0};
+        s_job[j] = RingJob(lane, F, fcnt, dp);
       }
       order();
 #pragma clang loop unroll(disable)
@@ -968,10 +979,10 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
         if (jj < total) {
           const RingJob jb = s_job[jj];
           if (16 * w < jb.cnt) {
-            const u32x4 v = lrd16(s_out + jb.lane * kOutStride + 16 +
+            const u32x4 v = lrd16(s_out + jb.lane() * kOutStride + 16 +
                                   ((jb.off + 16 * w) & (kOutRing - 1)));
             const gptr<uint8_t> g =
-                (gptr<uint8_t>)(((uint64_t)jb.phi << 32) | jb.plo) + jb.off + 16 * w;
+                (gptr<uint8_t>)jb.ptr() + jb.off + 16 * w;
             if (16 * w + 16 <= jb.cnt) st16(g, v);
             else st_exact(g, v, jb.cnt - 16 * w);
           }
@@ -1002,7 +1013,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       const uint32_t total = uni((uint32_t)__builtin_popcountll(m));
       if (need && j < 32) {
         const uint64_t sp = reinterpret_cast<uint64_t>(src);
-        s_job[j] = RingJob{lane, in_req, slen, (uint32_t)sp, (uint32_t)(sp >> 32), 0, 0, 0};
+        s_job[j] = RingJob(lane, in_req, slen, sp);
       }
       order();
       ra0 = rm0 = ra1 = rm1 = sink;
@@ -1010,19 +1021,19 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       if ((lane >> 2) < total) {
         const RingJob jb = s_job[lane >> 2];
         const uint32_t o = jb.off + 16 * w;
-        const gptr<const uint8_t> g = (gptr<const uint8_t>)(((uint64_t)jb.phi << 32) | jb.plo);
+        const gptr<const uint8_t> g = (gptr<const uint8_t>)jb.ptr();
         if (o < jb.cnt) rv0 = ld16(g + o);
         const uint32_t r = o & (kInRing - 1);
-        ra0 = jb.lane * kInStride + r;
+        ra0 = jb.lane() * kInStride + r;
         rm0 = r < 64 ? ra0 + kInRing : sink;
       }
       if (16 + (lane >> 2) < total) {
         const RingJob jb = s_job[16 + (lane >> 2)];
         const uint32_t o = jb.off + 16 * w;
-        const gptr<const uint8_t> g = (gptr<const uint8_t>)(((uint64_t)jb.phi << 32) | jb.plo);
+        const gptr<const uint8_t> g = (gptr<const uint8_t>)jb.ptr();
         if (o < jb.cnt) rv1 = ld16(g + o);
         const uint32_t r = o & (kInRing - 1);
-        ra1 = jb.lane * kInStride + r;
+        ra1 = jb.lane() * kInStride + r;
         rm1 = r < 64 ? ra1 + kInRing : sink;
       }
       order();
