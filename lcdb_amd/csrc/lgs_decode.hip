@@ -754,13 +754,13 @@ __device__ __forceinline__ u32x4 lrd16(const uint8_t* p) { return *(const u32x4_
 __device__ __forceinline__ void lwr16(uint8_t* p, u32x4 v) { *(u32x4_l1*)p = v; }
 
 // 16 bytes at output offset p of a lane's ring (ob = ring start): the ring
-// copy, plus the mirror copy (r < 64) or the wrapped part (r > 240); lanes
-// with neither write the pad in front of the ring.
+// copy, plus the mirror copy (r < 64) or the wrapped part (r > 240), which
+// only those lanes write.
 __device__ __forceinline__ void out_put(uint8_t* ob, uint32_t p, u32x4 v) {
   const uint32_t r = p & (ring::kOutRing - 1);
   lwr16(ob + r, v);
   const int32_t r2 = r < 64 ? (int32_t)r + 256 : (r > 240 ? (int32_t)r - 256 : -16);
-  lwr16(ob + r2, v);
+  if (r < 64 || r > 240) lwr16(ob + r2, v);
 }
 
 // A cooperative job (a refill or a flush) of one lane, 16 bytes: the lane
