@@ -950,10 +950,12 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       orem = 0;
       ofar = false;
     }
-    lwr16(s_in + ra0, rv0);
-    lwr16(s_in + rm0, rv0);
-    lwr16(s_in + ra1, rv1);
-    lwr16(s_in + rm1, rv1);
+    // (Lanes without a refill chunk, or a chunk without a mirror copy, hold
+    // the sink: they skip the write.)
+    if (ra0 != sink) lwr16(s_in + ra0, rv0);
+    if (rm0 != sink) lwr16(s_in + rm0, rv0);
+    if (ra1 != sink) lwr16(s_in + ra1, rv1);
+    if (rm1 != sink) lwr16(s_in + rm1, rv1);
     order();
     in_have = in_req;
 
