@@ -877,8 +877,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           // A literal reads the input window, a copy the output ring.
           const uint8_t* sp = lit ? ib + (olp & (kInRing - 1))
                                   : ob + ((made - dist) & (kOutRing - 1));
-          const u32x4 c0 = lrd16(sp), c1 = lrd16(sp + 16), c2 = lrd16(sp + 32),
-                      c3 = lrd16(sp + 48);
+          const u32x4 c0 = lrd16(sp);
           // Period 1/2/4/8: the dist bytes before d as a 16-byte pattern.
           const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
           const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
@@ -886,9 +885,13 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           const uint32_t py = dist == 8 ? c0.y : px;
           const u32x4 pv = {px, py, px, py};
           out_put(ob, made, pat ? pv : c0);
-          if (piece > 16) out_put(ob, made + 16, pat ? pv : c1);
-          if (piece > 32) out_put(ob, made + 32, pat ? pv : c2);
-          if (piece > 48) out_put(ob, made + 48, pat ? pv : c3);
+          // Later chunks are read only when the piece has them (and not for
+          // a pattern).  A source chunk can share ring slots only with a
+          // later destination chunk (dist <= 240), so reading chunk k just
+          // before writing chunk k keeps every read ahead of its clobber.
+          if (piece > 16) out_put(ob, made + 16, pat ? pv : lrd16(sp + 16));
+          if (piece > 32) out_put(ob, made + 32, pat ? pv : lrd16(sp + 32));
+          if (piece > 48) out_put(ob, made + 48, pat ? pv : lrd16(sp + 48));
         }
         made += piece;
         orem -= piece;
