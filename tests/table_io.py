@@ -147,3 +147,38 @@ def filter_handle(metaindex: bytes, name: bytes = b"filter.leveldb.BuiltinBloomF
             size, _ = _varint(v, at, len(v), 64)
             return off, size
     return None
+
+
+def entry_offsets(contents: bytes) -> list[int]:
+    """Start offset of every entry of a well-formed block, in order."""
+    n = len(contents)
+    nr = struct.unpack_from("<I", contents, n - 4)[0]
+    limit = n - (1 + nr) * 4
+    out, at = [], 0
+    while at < limit:
+        out.append(at)
+        shared, at2 = _varint(contents, at, limit, 32)
+        non_shared, at2 = _varint(contents, at2, limit, 32)
+        vlen, at2 = _varint(contents, at2, limit, 32)
+        at = at2 + non_shared + vlen
+    return out
+
+
+def with_raw_index(file: bytes, index_off: int, metaindex, contents: bytes) -> bytes:
+    """The table file with its index block replaced by `contents`, stored raw
+    (type 0, masked CRC32C trailer, table_builder.c:123-153) at the old
+    index offset, and a footer pointing at it (format.c:92-106)."""
+    import oracle
+
+    def v(x):
+        out = bytearray()
+        while x >= 128:
+            out.append((x & 127) | 128)
+            x >>= 7
+        out.append(x)
+        return bytes(out)
+    crc = oracle.crc32c_mask(oracle.crc32c(b"\x00", oracle.crc32c(contents)))
+    block = contents + b"\x00" + crc.to_bytes(4, "little")
+    handles = v(metaindex[0]) + v(metaindex[1]) + v(index_off) + v(len(contents))
+    footer = handles + b"\x00" * (40 - len(handles)) + (0xdb4775248b80fb57).to_bytes(8, "little")
+    return file[:index_off] + block + footer

@@ -6,6 +6,7 @@ ldb_read_block results (oracle/harness)."""
 from __future__ import annotations
 
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -266,6 +267,47 @@ def test_table_index_damaged_files(tab, ref_tables):
     # A cap too small is an error, not a truncated answer.
     with pytest.raises(Exception):
         tab.index_host(file, cap=ndata - 1)
+
+
+def test_table_index_corrupt_entries_vs_reference(tab, ref_tables, tmp_path):
+    """Index blocks with damaged entries (stored raw with a valid checksum, so
+    the block reads): the walk stops where lcdb's own block iterator stops
+    (block.c:80-126, 255-297), with the same handles before it."""
+    path, file, d = ref_tables[256]
+    contents = d.contents[-1]
+    io_ = d.index[0]
+    offs = table_io.entry_offsets(contents)
+    nr = struct.unpack_from("<I", contents, len(contents) - 4)[0]
+    cases = {}
+    k = len(offs) // 2
+    b = bytearray(contents)
+    b[offs[k]] = 0x7f                                    # shared > the previous key's size
+    cases["shared"] = bytes(b)
+    b = bytearray(contents)
+    b[offs[k] + 2] = 0x7f                                # value runs into the restart array
+    cases["value_len"] = bytes(b)
+    b = bytearray(contents)
+    b[offs[-1] + 1] = 0xff                               # an unterminated varint at the end
+    b[offs[-1] + 2] = 0xff
+    cases["varint"] = bytes(b)
+    b = bytearray(contents)
+    struct.pack_into("<I", b, len(b) - 4, 0)             # no restarts: an empty block
+    cases["no_restarts"] = bytes(b)
+    b = bytearray(contents)
+    struct.pack_into("<I", b, len(b) - 4, len(b))        # more restarts than fit
+    cases["restarts"] = bytes(b)
+    cases["intact_raw"] = contents
+    for name, cont in cases.items():
+        img = table_io.with_raw_index(file, io_, d.metaindex, cont)
+        p = tmp_path / f"{name}.ldb"
+        p.write_bytes(img)
+        ref = table_io.dump_blocks(str(p), str(tmp_path / f"{name}.bin"), True)
+        want = list(zip(ref.off[:ref.n - 2].tolist(), ref.size[:ref.n - 2].tolist()))
+        handles, keys, _, st = tab.index_host(img, True, internal_keys=False)
+        assert handles == want, name
+        ok = name in ("no_restarts", "intact_raw")
+        assert st == (tab.LGS_ST_OK if ok else tab.LGS_ST_CORRUPT), (name, st)
+    assert nr > 1
 
 
 def test_host_paths_chunked_c2_scale(tab):
