@@ -962,11 +962,21 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     order();
     in_have = in_req;
 
-    // ---- flush: 128 finished bytes, or the block's last bytes once the
-    // stream is consumed (snappy.c:337: it must end exactly at want).
+    // ---- flush finished bytes; the block's last ones once the stream is
+    // consumed (snappy.c:337: it must end exactly at want).
     if (st == 1 && orem == 0 && pos >= slen && made != want) st = 0;
     const bool fin = st == 1 && orem == 0 && pos >= slen;
-    const uint32_t fcnt = made - F >= kFlush ? kFlush : (fin ? made - F : 0u);
+    // Flush whole 128-byte lines of the destination: up to the last line
+    // boundary at or below dst + made, so every interior line is written by
+    // one job, once (a block's first and last lines are shared with its
+    // neighbours), then the tail after the last boundary once the block is
+    // finished.  A trip makes <= 128 bytes and F sits on a boundary (or at
+    // the block's start, before its first one), so a job is <= 128 bytes
+    // and D = made - F < 128 after the flush.
+    const uint64_t dpa = reinterpret_cast<uint64_t>(dst);
+    const uint64_t lb = (dpa + made) & ~(uint64_t)(kFlush - 1);
+    const uint32_t lim = lb > dpa ? (uint32_t)(lb - dpa) : 0u;
+    const uint32_t fcnt = lim > F ? lim - F : (fin ? made - F : 0u);
     {
       const bool need = st == 1 && fcnt > 0;
       const uint64_t m = ballot(need);
