@@ -141,8 +141,17 @@ __device__ uint32_t decode_stream(const Src& src, uint32_t slen, uint8_t* o,
 // each tag's 8-byte view is two v_readlane + a 64-bit shift into SGPRs.  The
 // window is refilled (one ds_read_b32 per lane) every ~250 stream bytes.
 // Only the byte moves touch LDS, one read + one write per tag.
+//
+// In place: the stream is staged at the top of the same LDS buffer the output
+// grows into from the bottom, o + gap == base.  Every write must end at or
+// below the next unread stream byte (made + len <= gap + next), so no byte is
+// overwritten before it is read; a stream that would break this (its output
+// running ahead of its input by more than the class margin) returns 3 and is
+// decoded again from global memory.  A literal needs made <= gap + from: its
+// lanes read a 64-byte piece before writing it, and each piece's writes end
+// where that piece's reads began, below every later piece.
 __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, uint8_t* o,
-                               uint32_t cap, uint32_t* want_out) {
+                               int32_t gap, uint32_t cap, uint32_t* want_out) {
   const uint32_t lane = lane_id();
   const uint32_t* b32 = reinterpret_cast<const uint32_t*>(base);
   uint32_t wbase = sh >> 2;
@@ -198,6 +207,7 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
       const uint32_t len = m + 1;
       if (len > want - made || len > left - hl) return 0;   // snappy.c:263
       const uint32_t from = apos + hl;
+      if ((int32_t)made - (int32_t)from > gap) return 3;
       if (len <= kWave) {
         if (lane < len) o[made + lane] = base[from + lane];
       } else {
@@ -229,6 +239,7 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
     apos += hl;
     if (dist == 0 || dist >= 0x80000000u) return 0;   // snappy.c:320
     if (made < dist || len > want - made) return 0;   // snappy.c:323
+    if ((int32_t)(made + len) - (int32_t)apos > gap) return 3;
     // len <= 64.  dist >= len: a plain move.  dist < len (rare): the
     // reference's forward byte loop repeats the dist-byte pattern.
     if (dist >= len) {
@@ -566,17 +577,22 @@ __global__ __launch_bounds__(64) void decode_lane_kernel(
   out_len[i] = st == 1 ? want : 0;
 }
 
-template <uint32_t OUT_CAP, uint32_t IN_CAP, uint32_t WAVES>
+template <uint32_t OUT_CAP, uint32_t WAVES>
 __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
     const uint32_t* __restrict__ index, uint32_t n) {
-  // s_in: + 48 for the alignment shift and zero pad, + 256 so the VGPR
-  // window of decode_lds never reads past this array.
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48 + 256];
-  __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][OUT_CAP + 32];
+  // One in-place buffer per wave: the output image grows from the bottom,
+  // the compressed stream is staged at the top (+ 48 for its alignment
+  // shift and zero pad, + 256 so the VGPR window of decode_lds never reads
+  // past the array).  kMargin is how far the output may run ahead of the
+  // input (literal headers still unread); half the LDS of separate
+  // input and output images, so twice the waves per CU.
+  constexpr uint32_t kMargin = 512 + OUT_CAP / 64;
+  constexpr uint32_t kBuf = (OUT_CAP + 32 + kMargin + 48 + 256 + 15) & ~15u;
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[WAVES][kBuf];
 
   // Per-wave scalars go through v_readfirstlane so hipcc keeps the whole
   // tag walk on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
@@ -590,17 +606,18 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   const gptr<uint8_t> dst = to_global(out) + uni64(out_off[i]);
   const uint32_t cap = uni(out_cap[i] < OUT_CAP ? out_cap[i] : OUT_CAP);
   const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
-  uint8_t* o = &s_out[wv][oshift];
+  uint8_t* o = &s_buf[wv][oshift];
 
-  uint32_t want = 0, st;
-  if (slen <= IN_CAP) {
-    const uint32_t sh = stage_in(&s_in[wv][0], src, slen);
+  uint32_t want = 0, st = 3;
+  if (slen <= kBuf - 48 - 256) {
+    const uint32_t ib = (kBuf - slen - 48 - 256) & ~15u;
+    const uint32_t sh = stage_in(&s_buf[wv][ib], src, slen);
     order();
-    st = decode_lds(&s_in[wv][0], sh, slen, o, cap, &want);
-  } else {
-    st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
+    st = decode_lds(&s_buf[wv][ib], sh, slen, o, (int32_t)ib - (int32_t)oshift, cap, &want);
+    order();
   }
-  if (st == 1) flush_out(dst, &s_out[wv][0], want);
+  if (st == 3) st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
+  if (st == 1) flush_out(dst, &s_buf[wv][0], want);
   if (lane_id() == 0) {
     status[i] = (uint8_t)st;
     out_len[i] = st == 1 ? want : 0;
@@ -704,10 +721,10 @@ __global__ __launch_bounds__(64) void decode_big_kernel(
 // ---------------------------------------------------------------------------
 namespace lgs {
 
-template <uint32_t OUT_CAP, uint32_t IN_CAP, uint32_t WAVES>
+template <uint32_t OUT_CAP, uint32_t WAVES>
 static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
   const uint32_t grid = (a.n + WAVES - 1) / WAVES;
-  hipLaunchKernelGGL((decode_kernel<OUT_CAP, IN_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
+  hipLaunchKernelGGL((decode_kernel<OUT_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
                      a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
                      a.index, a.n);
   return hipGetLastError();
@@ -1110,9 +1127,9 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   } else if (a.n >= kLaneMinBlocks) {
     return launch_decode_ring(a, s);
   }
-  if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 5632, 1>(a, s);
-  if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 19968, 1>(a, s);
-  if (max_out <= kDecCap2) return launch_decode_cls<kDecCap2, 76800, 1>(a, s);
+  if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
+  if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 1>(a, s);
+  if (max_out <= kDecCap2) return launch_decode_cls<kDecCap2, 1>(a, s);
   hipLaunchKernelGGL(decode_big_kernel, dim3(a.n), dim3(64), 0, s, a.in, a.in_off, a.in_len,
                      a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
   return hipGetLastError();

@@ -291,3 +291,49 @@ def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, monkeypatch, kernel):
     host = out2.buf.cpu().numpy()
     ref = np.concatenate([np.frombuffer(c.block(k), dtype=np.uint8) for k in range(c.n)])
     assert np.array_equal(host[3:3 + len(ref)], ref)
+
+
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def _runahead_stream(want: int, copy_frac: float) -> bytes:
+    # Output running ahead of input: 64-byte COPY2s (3 stream bytes each)
+    # first, then 1-byte literals (2 stream bytes each).  The wave decoder
+    # stages the stream at the top of its in-place LDS buffer; this shape
+    # breaks the in-place bound when the copies are many, and must then be
+    # decoded again from global memory, with the reference's result.
+    ncopy = int((want - 4) * copy_frac) // 64
+    nlit = want - 4 - 64 * ncopy
+    s = bytearray(_varint(want))
+    s += bytes([3 << 2]) + b"abcd"
+    s += bytes([(63 << 2) | 2, 4, 0]) * ncopy
+    for k in range(nlit):
+        s += bytes([0, 0x41 + k % 26])
+    return bytes(s)
+
+
+@pytest.mark.parametrize("kernel", [None, "ring"])
+def test_decode_in_place_runahead(gpu, kernel, monkeypatch):
+    # One batch per output size, so each LDS class of the wave decoder (4, 16
+    # and 64 KiB, chosen by the largest capacity) is the one that runs.
+    if kernel:
+        monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+    ref = oracle.best()
+    for want in (4000, 4600, 16000, 16800, 60000, 66000):
+        streams = []
+        for frac in (0.1, 0.5, 0.9, 0.97):
+            s = _runahead_stream(want, frac)
+            streams += [s, s[:-1], s[:-2] + bytes([0xFC])]   # ok, truncated, bad tail
+        res, st = gpu.decode_batch_host(streams, [want] * len(streams))
+        for k, (s, o, code) in enumerate(zip(streams, res, st)):
+            exp = ref.decode(s)
+            if exp is None:
+                assert code == gpu.LGS_ST_CORRUPT, (want, k)
+            else:
+                assert code == gpu.LGS_ST_OK and o == exp, (want, k)
