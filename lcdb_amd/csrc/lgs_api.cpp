@@ -349,7 +349,7 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
 
   EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
                (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen),
-               (const uint32_t*)(d + o_hdr), nullptr, nit};
+               (const uint32_t*)(d + o_hdr), nullptr, nit, nullptr};
   LGS_HIP(launch_encode(a, single ? n : kChunk, c.stream));
 
   uint32_t* olen = (uint32_t*)(h + o_olen);
@@ -416,7 +416,7 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
   DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
                (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
-               (uint32_t*)(d + o_olen), d + o_st, nullptr, 1};
+               (uint32_t*)(d + o_olen), d + o_st, nullptr, 1, nullptr};
   LGS_HIP(launch_decode(a, want, c.stream));
   LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
@@ -477,7 +477,7 @@ int lgs_encode_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const ui
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len)
     return fail(LGS_EINVAL, "NULL argument");
   if (max_in_len > 0x7fffffffu) return fail(LGS_EINVAL, "max_in_len %u too large", max_in_len);
-  EncodeArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nullptr, nullptr, n};
+  EncodeArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nullptr, nullptr, n, nullptr};
   LGS_HIP(launch_encode(a, max_in_len, (hipStream_t)stream));
   return LGS_OK;
 }
@@ -491,7 +491,7 @@ int lgs_decode_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const ui
       !d_status)
     return fail(LGS_EINVAL, "NULL argument");
   DecodeArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap, d_out_len, d_status,
-               nullptr, n};
+               nullptr, n, nullptr};
   LGS_HIP(launch_decode(a, max_out_cap, (hipStream_t)stream));
   return LGS_OK;
 }
@@ -539,7 +539,7 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   });
   LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
   EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
-               (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen), nullptr, nullptr, n};
+               (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen), nullptr, nullptr, n, nullptr};
   LGS_HIP(launch_encode(a, max_in, c.stream));
   LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, down_end - o_olen, hipMemcpyDeviceToHost,
                          c.stream));
@@ -602,7 +602,7 @@ int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
   DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
                (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
-               (uint32_t*)(d + o_olen), d + o_st, nullptr, n};
+               (uint32_t*)(d + o_olen), d + o_st, nullptr, n, nullptr};
   LGS_HIP(launch_decode(a, max_cap, c.stream));
   LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
@@ -671,7 +671,7 @@ int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const uint32_t*
   const bool snappy = compression == LGS_SNAPPY_COMPRESSION;
   if (snappy) {                       // table_builder.c:176-188, every block at once
     LGS_HIP(launch_scan(0, d_raw_len, nullptr, part, 0, enc_off, nullptr, n, s));
-    EncodeArgs a{d_raw, d_raw_off, d_raw_len, enc, enc_off, enc_len, nullptr, nullptr, n};
+    EncodeArgs a{d_raw, d_raw_off, d_raw_len, enc, enc_off, enc_len, nullptr, nullptr, n, nullptr};
     LGS_HIP(launch_encode(a, max_raw_len, s));
   }
   // File offsets of the framed blocks (table_builder.c:150), then the blocks.
@@ -698,7 +698,7 @@ int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* d_hoff,
   CheckArgs c{d_file, file_len, d_hoff, d_hsize, verify ? 1u : 0u, d_out, d_out_off, d_out_cap,
               d_out_len, d_status, dec_in_off, dec_len, dec_off, dec_cap, dummy_off, n};
   LGS_HIP(launch_check(c, s));
-  DecodeArgs d{d_file, dec_in_off, dec_len, d_out, dec_off, dec_cap, dec_olen, dec_st, nullptr, n};
+  DecodeArgs d{d_file, dec_in_off, dec_len, d_out, dec_off, dec_cap, dec_olen, dec_st, nullptr, n, nullptr};
   LGS_HIP(launch_decode(d, max_out_cap, s));
   LGS_HIP(launch_merge(d_status, d_out_len, dec_st, dec_olen, n, s));
   return LGS_OK;

@@ -583,7 +583,8 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
-    const uint32_t* __restrict__ index, uint32_t n) {
+    const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
   // One in-place buffer per wave: the output image grows from the bottom,
   // the compressed stream is staged at the top (+ 48 for its alignment
   // shift and zero pad, + 256 so the VGPR window of decode_lds never reads
@@ -598,7 +599,7 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   // tag walk on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
   const uint32_t wv = uni(threadIdx.x >> 6);
   const uint32_t slot = blockIdx.x * WAVES + wv;
-  if (slot >= n) return;
+  if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
 
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
@@ -639,9 +640,10 @@ __global__ __launch_bounds__(64) void decode_big_kernel(
     const uint32_t* __restrict__ in_len, uint8_t* out,
     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
-    const uint32_t* __restrict__ index, uint32_t n) {
+    const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
   const uint32_t slot = blockIdx.x;
-  if (slot >= n) return;
+  if (slot >= (count ? *count : n)) return;
   const uint32_t i = index ? index[slot] : slot;
   const uint32_t lane = lane_id();
   const GlobalStream src{to_global(in) + in_off[i], in_len[i]};
@@ -726,7 +728,7 @@ static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
   const uint32_t grid = (a.n + WAVES - 1) / WAVES;
   hipLaunchKernelGGL((decode_kernel<OUT_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
                      a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
-                     a.index, a.n);
+                     a.index, a.n, a.count);
   return hipGetLastError();
 }
 
@@ -798,7 +800,8 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
-    const uint32_t* __restrict__ index, uint32_t n) {
+    const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
   using namespace ring;
   // BL lanes decode (BL blocks per wave); with BL < 64 the others only help
   // with refills and flushes.  At most BL lanes post a flush job and at most
@@ -812,6 +815,8 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   // cooperative refills and flushes.
   const uint32_t lane = threadIdx.x;
   const uint32_t slot = blockIdx.x * BL + lane;
+  if (count) n = *count;
+  if (blockIdx.x * BL >= n) return;   // a whole wave without blocks
   const bool exists = lane < BL && slot < n;
   const uint32_t i = exists ? (index ? index[slot] : slot) : 0;
   const gptr<const uint8_t> src = to_global(in) + (exists ? in_off[i] : 0);
@@ -1088,15 +1093,15 @@ hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
   if (v && !strcmp(v, "ring1"))
     hipLaunchKernelGGL((decode_ring_kernel<false, 64>), dim3((a.n + 63) / 64), dim3(64), 0, s,
                        a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
-                       a.status, a.index, a.n);
+                       a.status, a.index, a.n, a.count);
   else if (v && !strcmp(v, "ring64"))
     hipLaunchKernelGGL((decode_ring_kernel<true, 64>), dim3((a.n + 63) / 64), dim3(64), 0, s,
                        a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
-                       a.status, a.index, a.n);
+                       a.status, a.index, a.n, a.count);
   else
     hipLaunchKernelGGL((decode_ring_kernel<true, 32>), dim3((a.n + 31) / 32), dim3(64), 0, s,
                        a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
-                       a.status, a.index, a.n);
+                       a.status, a.index, a.n, a.count);
   return hipGetLastError();
 }
 
@@ -1116,9 +1121,93 @@ static hipError_t launch_decode_lane(const DecodeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Mixed-size batches.  One launch sized for its largest block runs every
+// block in that class's LDS image (a 4 KiB block in a 64 KiB wave: two waves
+// per CU) or, in the ring decoder, lets one lane walk a 64 KiB block while
+// the rest of the chip idles.  So a batch whose largest block is over the
+// smallest class is first sorted into classes on the device, and each class
+// runs in its own kernel over its index list; the device-side count ends
+// the grid's surplus waves at once.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void classify_kernel(const uint32_t* __restrict__ len,
+                                                       uint32_t n, uint32_t b0, uint32_t b1,
+                                                       uint32_t b2, uint32_t* __restrict__ list,
+                                                       uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const bool here = i < n;
+  const uint32_t v = here ? len[i] : 0;
+  const uint32_t c = v <= b0 ? 0 : v <= b1 ? 1 : v <= b2 ? 2 : 3;
+  const uint32_t lane = lane_id();
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint64_t m = __ballot(here && c == k);
+    if (m == 0) continue;
+    const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[k], (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (here && c == k) list[(size_t)k * n + base + __popcll(m & ((1ull << lane) - 1))] = i;
+  }
+}
+
+hipError_t launch_classify(const uint32_t* len, uint32_t n, uint32_t b0, uint32_t b1, uint32_t b2,
+                           uint32_t* list, uint32_t* cnt, hipStream_t s) {
+  hipLaunchKernelGGL(classify_kernel, dim3((n + 255) / 256), dim3(256), 0, s, len, n, b0, b1, b2,
+                     list, cnt);
+  return hipGetLastError();
+}
+
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
+  // Keep freed blocks in the device's default pool, so a split launch does
+  // not map memory every time.
+  static thread_local int tuned = -1;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (tuned != dev) {
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    tuned = dev;
+  }
+  return hipMallocAsync(p, bytes, s);
+}
+
+#define LGS_TRY(x) do { const hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
+
+static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
+  void* scratch = nullptr;
+  const size_t list_bytes = (size_t)4 * a.n * sizeof(uint32_t);
+  LGS_TRY(scratch_alloc(&scratch, list_bytes + 16, s));
+  uint32_t* list = (uint32_t*)scratch;
+  uint32_t* cnt = (uint32_t*)((uint8_t*)scratch + list_bytes);
+  LGS_TRY(hipMemsetAsync(cnt, 0, 16, s));
+  LGS_TRY(launch_classify(a.out_cap, a.n, kDecCap0, kDecCap1, kDecCap2, list, cnt, s));
+  DecodeArgs c = a;
+  c.index = list; c.count = cnt;
+  LGS_TRY((a.n >= kLaneMinBlocks ? launch_decode_ring(c, s) : launch_decode_cls<kDecCap0, 1>(c, s)));
+  c.index = list + a.n; c.count = cnt + 1;
+  LGS_TRY((launch_decode_cls<kDecCap1, 1>(c, s)));
+  if (max_out > kDecCap1) {            // (classes above max_out are empty)
+    c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
+    LGS_TRY((launch_decode_cls<kDecCap2, 1>(c, s)));
+  }
+  if (max_out > kDecCap2) {
+    c.index = list + 3 * (size_t)a.n; c.count = cnt + 3;
+    hipLaunchKernelGGL(decode_big_kernel, dim3(a.n), dim3(64), 0, s, c.in, c.in_off, c.in_len,
+                       c.out, c.out_off, c.out_cap, c.out_len, c.status, c.index, c.n, c.count);
+    LGS_TRY(hipGetLastError());
+  }
+  return hipFreeAsync(scratch, s);
+}
+
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const char* force = getenv("LGS_DECODE_KERNEL");   // "ring" | "wave" | "lane64" | ...
+  if (!force && !a.index && max_out > kDecCap0 && !getenv("LGS_NO_SPLIT"))
+    return launch_decode_split(a, max_out, s);
   if (force) {
     if (!strncmp(force, "ring", 4)) return launch_decode_ring(a, s);
     if (!strcmp(force, "lane64")) return launch_decode_lane<64>(a, s);
@@ -1131,7 +1220,7 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 1>(a, s);
   if (max_out <= kDecCap2) return launch_decode_cls<kDecCap2, 1>(a, s);
   hipLaunchKernelGGL(decode_big_kernel, dim3(a.n), dim3(64), 0, s, a.in, a.in_off, a.in_len,
-                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
+                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n, a.count);
   return hipGetLastError();
 }
 

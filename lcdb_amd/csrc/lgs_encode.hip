@@ -534,7 +534,8 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
-    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n) {
+    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
   __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
   __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap + 8];   // + sink
 
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   // flow on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
   const uint32_t wv = uni(threadIdx.x >> 6);
   const uint32_t slot = blockIdx.x * WAVES + wv;
-  if (slot >= n) return;
+  if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
   // Probe offsets of search probes pi - 2 (the batch right after a copy,
@@ -611,10 +612,12 @@ static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
   const char* emit = getenv("LGS_ENCODE_EMIT");
   if (emit && !strcmp(emit, "inline")) {
     hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES, false>), dim3(grid), dim3(64 * WAVES), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n);
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
+                       a.count);
   } else {
     hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES, true>), dim3(grid), dim3(64 * WAVES), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n);
+                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
+                       a.count);
   }
   return hipGetLastError();
 }
@@ -634,8 +637,30 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
     if (e != hipErrorNotSupported) return e;
   }
   if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
-  if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
-  return launch_encode_cls<kEncCap2, 1>(a, s);
+  if (a.index || getenv("LGS_NO_SPLIT")) {
+    if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
+    return launch_encode_cls<kEncCap2, 1>(a, s);
+  }
+  // A mixed-size batch: each size class in its own kernel (see
+  // launch_decode_split), so small blocks keep their small LDS images.
+  void* scratch = nullptr;
+  const size_t list_bytes = (size_t)3 * a.n * sizeof(uint32_t);
+  hipError_t e = scratch_alloc(&scratch, list_bytes + 16, s);
+  if (e != hipSuccess) return e;
+  uint32_t* list = (uint32_t*)scratch;
+  uint32_t* cnt = (uint32_t*)((uint8_t*)scratch + list_bytes);
+  EncodeArgs c = a;
+  if ((e = hipMemsetAsync(cnt, 0, 16, s)) != hipSuccess ||
+      (e = launch_classify(a.in_len, a.n, kEncCap0, kEncCap1, 0xffffffffu, list, cnt, s)) !=
+          hipSuccess)
+    return e;
+  c.index = list; c.count = cnt;
+  if ((e = launch_encode_cls<kEncCap0, 1>(c, s)) != hipSuccess) return e;
+  c.index = list + a.n; c.count = cnt + 1;
+  if ((e = launch_encode_cls<kEncCap1, 1>(c, s)) != hipSuccess) return e;
+  c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
+  if (max_in > kEncCap1 && (e = launch_encode_cls<kEncCap2, 1>(c, s)) != hipSuccess) return e;
+  return hipFreeAsync(scratch, s);
 }
 
 hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,

@@ -13,12 +13,14 @@ struct DecodeArgs {
   const uint8_t* in; const uint64_t* in_off; const uint32_t* in_len;
   uint8_t* out; const uint64_t* out_off; const uint32_t* out_cap;
   uint32_t* out_len; uint8_t* status; const uint32_t* index; uint32_t n;
+  const uint32_t* count;   // device count of index[] entries (nullptr: n)
 };
 
 struct EncodeArgs {
   const uint8_t* in; const uint64_t* in_off; const uint32_t* in_len;
   uint8_t* out; const uint64_t* out_off; uint32_t* out_len;
   const uint32_t* hdr; const uint32_t* index; uint32_t n;
+  const uint32_t* count;   // device count of index[] entries (nullptr: n)
 };
 
 // max_out: largest out_cap in the launch (selects the LDS class).
@@ -29,6 +31,14 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s);
 // 16, 32 or 64.  hipErrorNotSupported if the batch does not qualify.
 hipError_t launch_encode_group(const EncodeArgs& a, uint32_t max_in, uint32_t lanes,
                                hipStream_t s);
+// Sort a mixed-size batch into size classes on the device: class c holds
+// the items with len in (b[c-1], b[c]] (b[3] = infinity); list[c * n + k]
+// is its k-th item (in no particular order), cnt[c] its size.  cnt must be
+// zeroed beforehand.
+hipError_t launch_classify(const uint32_t* len, uint32_t n, uint32_t b0, uint32_t b1, uint32_t b2,
+                           uint32_t* list, uint32_t* cnt, hipStream_t s);
+// Stream-ordered scratch for a split launch (one device's pool, kept warm).
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                          uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s);
 

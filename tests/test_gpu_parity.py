@@ -337,3 +337,35 @@ def test_decode_in_place_runahead(gpu, kernel, monkeypatch):
                 assert code == gpu.LGS_ST_CORRUPT, (want, k)
             else:
                 assert code == gpu.LGS_ST_OK and o == exp, (want, k)
+
+
+def test_split_launch_all_classes(gpu, monkeypatch):
+    # A batch mixing every size class, large enough (>= 16 384 blocks) that
+    # the 4 KiB class goes to the ring decoder: the launch is sorted into
+    # classes on the device, each class in its own kernel.  Compressed bytes
+    # equal the reference's (oracle, per block) and the unsplit launch's;
+    # the round trip is exact, every status ok.
+    import torch
+    from lcdb_amd import batch
+    ref = oracle.best()
+    c = corpus.concat(corpus.fillseq(16000), corpus.random_blocks(400, 4096),
+                      corpus.fillseq(40, block_size=16384), corpus.random_blocks(30, 16384),
+                      corpus.fillseq(12, block_size=65536), corpus.random_blocks(6, 65536),
+                      corpus.fillseq(3, block_size=100000), corpus.random_blocks(2, 70000))
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    out = batch.decode_slots(c.len)
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    batch.decode(comp, out, st)
+    torch.cuda.synchronize()
+    assert bool((st == 1).all())
+    assert batch.digest(out) == batch.digest(raw)
+    host = batch.to_host(comp)
+    for k in list(range(0, c.n, 97)) + list(range(c.n - 100, c.n)):
+        assert host.block(k) == ref.encode(c.block(k)), k
+    monkeypatch.setenv("LGS_NO_SPLIT", "1")
+    comp2 = batch.encode_slots(raw)
+    batch.encode(raw, comp2)
+    torch.cuda.synchronize()
+    assert batch.digest(comp2) == batch.digest(comp)
