@@ -1206,7 +1206,7 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const char* force = getenv("LGS_DECODE_KERNEL");   // "ring" | "wave" | "lane64" | ...
-  if (!force && !a.index && max_out > kDecCap0 && !getenv("LGS_NO_SPLIT"))
+  if (!force && !a.index && max_out > kDecCap0 && a.n >= kSplitMinBlocks && !getenv("LGS_NO_SPLIT"))
     return launch_decode_split(a, max_out, s);
   if (force) {
     if (!strncmp(force, "ring", 4)) return launch_decode_ring(a, s);

@@ -637,7 +637,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
     if (e != hipErrorNotSupported) return e;
   }
   if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
-  if (a.index || getenv("LGS_NO_SPLIT")) {
+  if (a.index || a.n < kSplitMinBlocks || getenv("LGS_NO_SPLIT")) {
     if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
     return launch_encode_cls<kEncCap2, 1>(a, s);
   }

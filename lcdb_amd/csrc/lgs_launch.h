@@ -35,6 +35,10 @@ hipError_t launch_encode_group(const EncodeArgs& a, uint32_t max_in, uint32_t la
 // the items with len in (b[c-1], b[c]] (b[3] = infinity); list[c * n + k]
 // is its k-th item (in no particular order), cnt[c] its size.  cnt must be
 // zeroed beforehand.
+// Below this many blocks a split gains nothing (each wave has a CU to
+// itself whatever its LDS class) and would only add its fixed cost to
+// latency-bound calls such as the drop-in's single blocks.
+constexpr uint32_t kSplitMinBlocks = 512;
 hipError_t launch_classify(const uint32_t* len, uint32_t n, uint32_t b0, uint32_t b1, uint32_t b2,
                            uint32_t* list, uint32_t* cnt, hipStream_t s);
 // Stream-ordered scratch for a split launch (one device's pool, kept warm).
