@@ -194,20 +194,24 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
     const uint32_t tag = (uint32_t)t & 0xffu;
     const uint32_t left = aend - apos;
 
+    // Each kind's reject conditions are folded into one flag (with the
+    // in-place bound) and tested by one branch: the walk is issue-bound, and
+    // a branch per condition cost more than the compares.
     if ((tag & 3u) == 0) {                          // literal, snappy.c:210-273
       uint32_t m = tag >> 2, hl = 1;
+      bool bad = false;
       if (m >= 60) {
         const uint32_t extra = m - 59;
-        if (left - 1 < extra) return 0;
+        bad = left - 1 < extra;
         const uint32_t hi = (uint32_t)(t >> 8);
         m = extra == 4 ? hi : (hi & ((1u << (8 * extra)) - 1u));
         hl += extra;
       }
-      if (m >= 0x7fffffffu) return 0;               // snappy.c:258
       const uint32_t len = m + 1;
-      if (len > want - made || len > left - hl) return 0;   // snappy.c:263
       const uint32_t from = apos + hl;
-      if ((int32_t)made - (int32_t)from > gap) return 3;
+      bad = bad | (m >= 0x7fffffffu) | (len > want - made) | (len > left - hl);  // :258, :263
+      const bool ahead = (int32_t)made - (int32_t)from > gap;
+      if (bad | ahead) return bad ? 0u : 3u;
       if (len <= kWave) {
         if (lane < len) o[made + lane] = base[from + lane];
       } else {
@@ -219,27 +223,18 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
       continue;
     }
 
-    uint32_t len, dist, hl;
-    if ((tag & 3u) == 1) {                          // COPY1, snappy.c:276-287
-      if (left < 2) return 0;
-      len = 4 + ((tag >> 2) & 7u);
-      dist = ((tag & 0xe0u) << 3) | ((uint32_t)(t >> 8) & 0xffu);
-      hl = 2;
-    } else if ((tag & 3u) == 2) {                   // COPY2, snappy.c:289-301
-      if (left < 3) return 0;
-      len = 1 + (tag >> 2);
-      dist = (uint32_t)(t >> 8) & 0xffffu;
-      hl = 3;
-    } else {                                        // COPY4, snappy.c:303-317
-      if (left < 5) return 0;
-      len = 1 + (tag >> 2);
-      dist = (uint32_t)(t >> 8);
-      hl = 5;
-    }
+    // COPY1 / COPY2 / COPY4, snappy.c:276-317
+    const uint32_t kind = tag & 3u;
+    const uint32_t hi = (uint32_t)(t >> 8);
+    const uint32_t hl = kind == 1 ? 2u : kind == 2 ? 3u : 5u;
+    const uint32_t len = kind == 1 ? 4 + ((tag >> 2) & 7u) : 1 + (tag >> 2);
+    const uint32_t dist = kind == 1 ? (((tag & 0xe0u) << 3) | (hi & 0xffu))
+                        : kind == 2 ? (hi & 0xffffu) : hi;
     apos += hl;
-    if (dist == 0 || dist >= 0x80000000u) return 0;   // snappy.c:320
-    if (made < dist || len > want - made) return 0;   // snappy.c:323
-    if ((int32_t)(made + len) - (int32_t)apos > gap) return 3;
+    const bool bad = (left < hl) | (dist == 0) | (dist >= 0x80000000u) |   // :320
+                     (made < dist) | (len > want - made);                  // :323
+    const bool ahead = (int32_t)(made + len) - (int32_t)apos > gap;
+    if (bad | ahead) return bad ? 0u : 3u;
     // len <= 64.  dist >= len: a plain move.  dist < len (rare): the
     // reference's forward byte loop repeats the dist-byte pattern.
     if (dist >= len) {
