@@ -210,10 +210,15 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
       const uint32_t len = m + 1;
       const uint32_t from = apos + hl;
       bad = bad | (m >= 0x7fffffffu) | (len > want - made) | (len > left - hl);  // :258, :263
-      const bool ahead = (int32_t)made - (int32_t)from > gap;
+      // (+ kWave: a short literal writes all 64 lanes, see below)
+      const bool ahead = (int32_t)(made + kWave) - (int32_t)from > gap;
       if (bad | ahead) return bad ? 0u : 3u;
       if (len <= kWave) {
-        if (lane < len) o[made + lane] = base[from + lane];
+        // Every lane moves a byte, so there is no exec-mask region: lanes
+        // past len write bytes past the op that later ops overwrite (the
+        // flush stops at want; the in-place bound above covers them).
+        const uint8_t v = base[from + lane];
+        o[made + lane] = v;
       } else {
         for (uint32_t j = lane; j < len; j += kWave) o[made + j] = base[from + j];
       }
@@ -233,15 +238,13 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
     apos += hl;
     const bool bad = (left < hl) | (dist == 0) | (dist >= 0x80000000u) |   // :320
                      (made < dist) | (len > want - made);                  // :323
-    const bool ahead = (int32_t)(made + len) - (int32_t)apos > gap;
+    const bool ahead = (int32_t)(made + kWave) - (int32_t)apos > gap;
     if (bad | ahead) return bad ? 0u : 3u;
     // len <= 64.  dist >= len: a plain move.  dist < len (rare): the
     // reference's forward byte loop repeats the dist-byte pattern.
-    if (dist >= len) {
-      if (lane < len) {
-        const uint8_t v = o[made - dist + lane];
-        o[made + lane] = v;
-      }
+    if (dist >= len) {                              // all 64 lanes, as for literals
+      const uint8_t v = o[made - dist + lane];
+      o[made + lane] = v;
     } else if (lane < len) {
       const uint8_t v = o[made - dist + lane % dist];
       o[made + lane] = v;
