@@ -229,12 +229,14 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
     }
 
     // COPY1 / COPY2 / COPY4, snappy.c:276-317
+    // Picked by masks, not ?: -- hipcc lowers these selects to branches.
     const uint32_t kind = tag & 3u;
     const uint32_t hi = (uint32_t)(t >> 8);
-    const uint32_t hl = kind == 1 ? 2u : kind == 2 ? 3u : 5u;
-    const uint32_t len = kind == 1 ? 4 + ((tag >> 2) & 7u) : 1 + (tag >> 2);
-    const uint32_t dist = kind == 1 ? (((tag & 0xe0u) << 3) | (hi & 0xffu))
-                        : kind == 2 ? (hi & 0xffffu) : hi;
+    const uint32_t k1 = 0u - (uint32_t)(kind == 1), k2 = 0u - (uint32_t)(kind == 2);
+    const uint32_t hl = (0x05030200u >> (8 * kind)) & 0xffu;
+    const uint32_t len = ((4 + ((tag >> 2) & 7u)) & k1) | ((1 + (tag >> 2)) & ~k1);
+    const uint32_t dist = ((((tag & 0xe0u) << 3) | (hi & 0xffu)) & k1) |
+                          (hi & (k2 ? 0xffffu : 0xffffffffu) & ~k1);
     apos += hl;
     const bool bad = (left < hl) | (dist == 0) | (dist >= 0x80000000u) |   // :320
                      (made < dist) | (len > want - made);                  // :323
