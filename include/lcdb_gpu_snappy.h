@@ -88,7 +88,12 @@ int lgs_encode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
    max_out_cap >= every d_out_cap[i].  Asynchronous on `stream`.
    Read slack: the kernel may READ (never write) up to 16 bytes past the end
    of a block's input and past its output cursor, so both allocations must
-   extend at least 16 bytes beyond the last block. */
+   extend at least 16 bytes beyond the last block.
+   Both _dev calls: a batch of >= 512 blocks whose largest block is over
+   4 608 bytes is sorted into size classes on the device first, with up to
+   16 bytes per block of stream-ordered scratch from the device's default
+   memory pool (hipMallocAsync, freed on `stream`); LGS_ENOMEM-class HIP
+   errors are possible there.  LGS_NO_SPLIT=1 turns this off. */
 int lgs_decode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
                          const uint32_t *d_in_len, uint8_t *d_out,
                          const uint64_t *d_out_off, const uint32_t *d_out_cap,
