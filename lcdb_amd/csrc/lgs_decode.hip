@@ -188,6 +188,11 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
   uint32_t apos = sh + hlen;                        // absolute LDS offset of the next tag
   const uint32_t aend = sh + slen;
   uint32_t made = 0;
+  // Deferred write: an op's byte is read from LDS, and written only after the
+  // next tag has been parsed, so the read's latency hides behind the parse.
+  // It is written before the next op reads anything (a copy may read it).
+  // Until the first op it aims at the stream's never-consumed pad.
+  uint32_t pend = (uint32_t)((int32_t)aend + gap) + kWave + lane, pv = 0;
 
   while (apos < aend) {                             // snappy.c:208
     const uint64_t t = view(apos);
@@ -213,15 +218,17 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
       // (+ kWave: a short literal writes all 64 lanes, see below)
       const bool ahead = (int32_t)(made + kWave) - (int32_t)from > gap;
       if (bad | ahead) return bad ? 0u : 3u;
+      o[pend] = (uint8_t)pv;
       if (len <= kWave) {
         // Every lane moves a byte, so there is no exec-mask region: lanes
         // past len write bytes past the op that later ops overwrite (the
         // flush stops at want; the in-place bound above covers them).
-        const uint8_t v = base[from + lane];
-        o[made + lane] = v;
+        pv = base[from + lane];
       } else {
         for (uint32_t j = lane; j < len; j += kWave) o[made + j] = base[from + j];
+        pv = o[made + lane];                        // (rewrites the same bytes)
       }
+      pend = made + lane;
       order();
       made += len;
       apos = from + len;
@@ -244,16 +251,17 @@ __device__ uint32_t decode_lds(const uint8_t* base, uint32_t sh, uint32_t slen, 
     if (bad | ahead) return bad ? 0u : 3u;
     // len <= 64.  dist >= len: a plain move.  dist < len (rare): the
     // reference's forward byte loop repeats the dist-byte pattern.
+    o[pend] = (uint8_t)pv;
     if (dist >= len) {                              // all 64 lanes, as for literals
-      const uint8_t v = o[made - dist + lane];
-      o[made + lane] = v;
-    } else if (lane < len) {
-      const uint8_t v = o[made - dist + lane % dist];
-      o[made + lane] = v;
+      pv = o[made - dist + lane];
+    } else {
+      pv = o[made - dist + lane % dist];            // lanes >= len: wild, overwritten later
     }
+    pend = made + lane;
     order();
     made += len;
   }
+  o[pend] = (uint8_t)pv;
 
   return made == want ? 1u : 0u;                    // snappy.c:337
 }
