@@ -2,29 +2,41 @@
 """bench.py -- device-resident Snappy encode+decode throughput on MI355X.
 
 Metric (BASELINE.json): device-resident GiB/s of Snappy encode+decode on
-4 KiB SSTable blocks.  One *step* = one encode launch + one decode launch over
-the GPU's whole batch of synthetic db_bench fillseq blocks (BASELINE config 2:
-65 536 x 4 KiB blocks per GPU), inputs already resident in HBM.
-``value`` = uncompressed bytes that went through encode AND decode, summed
-over all ranks, / wall time of the K timed steps (max over ranks), in GiB/s.
+4 KiB SSTable blocks at 1/2/4/8 MI355X.  One *step* = one encode launch + one
+decode launch over a GPU's whole share of synthetic db_bench fillseq blocks,
+inputs already resident in HBM.  ``value`` = uncompressed bytes that went
+through encode AND decode, summed over all ranks, / wall time of the K timed
+steps (max over ranks), in GiB/s.
 
-Multi-GPU (``torch.distributed.run``, one process per GPU): blocks are a
-round-robin partition of one fillseq stream (block g -> rank g % N), each
-rank holds 65 536 blocks (weak scaling); no data-path collective -- only the
-barrier and the max-over-ranks timing reduction.
+Workloads (BASELINE.json ``configs``):
+  * N = 1 (default): C2, 65 536 x 4 KiB blocks on one GPU.
+  * N > 1 (default): C4, 1 048 576 x 4 KiB blocks dealt round-robin
+    (block g -> rank g % N), strong scaling: each rank holds 1 048 576 / N.
+  * ``--total-blocks T`` picks any stream length (``--total-blocks 1048576``
+    at N = 1 is C4's one-GPU point).
+
+Multi-GPU: one process per GPU.  Under ``torch.distributed.run`` the ranks
+come from RANK / LOCAL_RANK / WORLD_SIZE, which must agree with ``--gpus``.
+Without them, ``--gpus N`` (N > 1) starts the N rank processes itself
+before anything touches a GPU (127.0.0.1 rendezvous) and exits with their
+status.  The process group is gloo: ranks only meet at the timing barriers,
+the max-over-ranks reduction and, after timing, the parity gather of
+per-block digests -- no data-path collective, no RCCL.
 
 Extra JSON fields: per-kernel HIP-event timings (``kernels``), the roofline
 of the dominant kernel (algorithmic bytes = raw + compressed + 16 per block,
-SURVEY §8d), the CPU baseline (reference snappy.c from oracle/_ref on a
-bounded sample, rank 0 at N=1 only), and a parity check of this run's output
-against the reference digest.
+SURVEY §8d), the CPU baseline (the reference snappy.c from oracle/_ref, rank 0
+at N = 1 only, BASELINE.md's plan: 1 thread and the host's thread share, same
+blocks, median of 5) and the parity of this run's output against the
+reference digests.
 """
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,51 +44,166 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+C2_BLOCKS, C4_BLOCKS = 65536, 1048576
 
 
-def parse() -> argparse.Namespace:
+def parse(argv=None) -> argparse.Namespace:
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--blocks", type=int, default=65536, help="blocks per GPU")
+    p.add_argument("--total-blocks", type=int, default=0,
+                   help="blocks in the whole stream, dealt round-robin over the ranks "
+                        "(0: C2 = 65 536 at N = 1, C4 = 1 048 576 at N > 1)")
+    p.add_argument("--blocks", type=int, default=0,
+                   help="blocks per GPU (weak scaling); overrides --total-blocks")
     p.add_argument("--block-size", type=int, default=4096)
     p.add_argument("--copies", type=int, default=2,
                    help="independent corpus copies rotated per step (defeats the 256 MiB MALL)")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpu_count)")
-    p.add_argument("--cpu-sample", type=int, default=16384, help="blocks in the CPU sample")
+    p.add_argument("--cpu-reps", type=int, default=5)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="the multi-thread CPU point (0: this host's CPU share, <= 16)")
+    p.add_argument("--cpu-sample", type=int, default=C2_BLOCKS,
+                   help="blocks in the CPU sample (the first of the GPU's blocks)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--no-pipelined", action="store_true",
                    help="skip the extra concurrent encode||decode measurement")
+    p.add_argument("--plan-only", action="store_true",
+                   help="no GPU: launch, partition and digest-gather only (CPU tests)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
-                   help="PMC traffic summary (written by tools/profile_traffic.py)")
-    return p.parse_args()
+                   help="PMC traffic summary (tools/traffic_json.py)")
+    return p.parse_args(argv)
 
 
-def main() -> None:
-    a = parse()
+def total_blocks(a, world: int) -> int:
+    if a.blocks:
+        return a.blocks * world
+    if a.total_blocks:
+        return a.total_blocks
+    return C2_BLOCKS if world == 1 else C4_BLOCKS
+
+
+def workload_name(total: int, a, world: int) -> str:
+    kib = a.block_size // 1024
+    if a.block_size == 4096 and not a.blocks:
+        if total == C2_BLOCKS and world == 1:
+            return f"C2: {total} x 4 KiB db_bench fillseq blocks on 1 GPU, encode+decode"
+        if total == C4_BLOCKS:
+            return (f"C4: {total} x 4 KiB db_bench fillseq blocks round-robin over {world} "
+                    f"GPU{'s' if world > 1 else ''}, encode+decode")
+    return (f"{total} x {kib} KiB db_bench fillseq blocks round-robin over {world} GPU(s), "
+            f"encode+decode")
+
+
+def reference_digest(total: int, a) -> dict | None:
+    """The pinned reference digests of this exact stream, if any."""
+    if a.block_size != 4096:
+        return None
+    dg = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    for key in ("C1_fillseq_1024x4KiB", "C2_fillseq_65536x4KiB", "C4_fillseq_1048576x4KiB"):
+        d = dg.get(key)
+        if d and d.get("blocks") == total and "comp_dd" in d:
+            return dict(d, name=key)
+    return None
+
+
+# ---------------------------------------------------------------- launcher
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Start n rank processes of this script (this process never touches a
+    GPU) and return the first non-zero exit status, else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+# ---------------------------------------------------------------- ranks
+
+def gather_digests(dist, rank: int, world: int, per_block: np.ndarray, total: int):
+    """Rank 0 receives every rank's per-block digests and puts them back in
+    global stream order (gloo, after the timed region)."""
+    from lcdb_amd import shard
+    if dist is None:
+        return per_block
+    got = [None] * world
+    dist.all_gather_object(got, per_block)
+    return shard.interleave(got, total) if rank == 0 else None
+
+
+def run_plan_only(a, rank: int, world: int, dist) -> None:
+    """Launcher + partition + digest path without a GPU: each rank builds its
+    shard; rank 0 reassembles the raw stream's digest-of-digests."""
+    from lcdb_amd import corpus, shard
+    total = total_blocks(a, world)
+    c = shard.fillseq_total(total, rank, world, a.block_size)
+    per = corpus.block_digests(c.buf, c.off, c.len)
+    allb = gather_digests(dist, rank, world, per, total)
+    tmax = shard.max_over_ranks(float(rank + 1), dist)
+    if rank == 0:
+        print(json.dumps({"plan_only": True, "n_gpus": world, "total_blocks": total,
+                          "blocks_rank0": c.n, "raw_dd": corpus.digest_of_digests(allb),
+                          "max_over_ranks": tmax,
+                          "workload": workload_name(total, a, world)}), flush=True)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return spawn_ranks(a.gpus, argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
+
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if a.plan_only:
+            run_plan_only(a, rank, world, dist)
+        else:
+            run(a, rank, world, local, dist)
+    finally:
+        if dist is not None:
+            dist.destroy_process_group()
+    return 0
 
-    from lcdb_amd import batch, shard, snappy  # noqa: F401  (loads the HIP library)
+
+def run(a, rank: int, world: int, local: int, dist) -> None:
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from lcdb_amd import batch, corpus, shard, snappy  # noqa: F401  (loads the HIP library)
+    from lcdb_amd.build import kernel_sources_sha
 
     baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    total = total_blocks(a, world)
 
-    # ---- workload: this rank's round-robin shard of one fillseq stream ----
+    # ---- workload: this rank's round-robin share of one fillseq stream ----
     t_gen = time.perf_counter()
-    c = shard.fillseq_shard(a.blocks, rank, world, a.block_size)
+    c = shard.fillseq_total(total, rank, world, a.block_size)
     t_gen = time.perf_counter() - t_gen
     n = c.n
     raw_bytes = c.raw_bytes
@@ -85,17 +212,18 @@ def main() -> None:
     comps = [batch.encode_slots(r) for r in raws]
     outs = [batch.decode_slots(c.len, dev) for _ in range(a.copies)]
     stats = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(a.copies)]
+    stream = torch.cuda.current_stream(dev)    # the stream the codec launches on
 
     def step(k: int, ev=None) -> None:
         j = k % a.copies
         if ev is not None:
-            ev[0].record()
-        batch.encode(raws[j], comps[j])
+            ev[0].record(stream)
+        batch.encode(raws[j], comps[j], stream)
         if ev is not None:
-            ev[1].record()
-        batch.decode(comps[j], outs[j], stats[j])
+            ev[1].record(stream)
+        batch.decode(comps[j], outs[j], stats[j], stream)
         if ev is not None:
-            ev[2].record()
+            ev[2].record(stream)
 
     for k in range(a.warmup):
         step(k)
@@ -112,7 +240,7 @@ def main() -> None:
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = shard.max_over_ranks(t1 - t0, dist, dev)
+    elapsed = shard.max_over_ranks(t1 - t0, dist)
 
     # ---- extra (not `value`): encode and decode concurrently on two streams,
     # step k encoding copy k while decoding what step k-1 encoded -- the shape
@@ -138,7 +266,7 @@ def main() -> None:
             batch.decode(comps[jp], outs[jp], stats[jp], s_dec)
             dec_done[jp].record(s_dec)
         torch.cuda.synchronize()
-        tp = shard.max_over_ranks(time.perf_counter() - t0p, dist, dev)
+        tp = shard.max_over_ranks(time.perf_counter() - t0p, dist)
         pipelined = {"GiBps": raw_bytes * world * a.steps / tp / 2**30,
                      "ms_per_step": tp / a.steps * 1e3,
                      "note": "encode(step k) || decode(step k-1) on two streams; extra field, "
@@ -148,61 +276,85 @@ def main() -> None:
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     comp_bytes = int(comps[0].len.sum(dtype=torch.int64).item())
 
-    # ---- parity of this run's output ----
+    # ---- parity of this run's output (after the timed region) ----
     parity = None
+    hc = None
     if not a.no_parity:
         ok = all(bool((s == 1).all()) for s in stats)
-        dec_sha, _ = batch.digest(outs[0])
-        ok = ok and dec_sha == c.sha256()
-        comp_sha, _ = batch.digest(comps[0])
-        ok = ok and all(batch.digest(x)[0] == comp_sha for x in comps[1:])
-        dg = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
-        ref = dg.get("C2_fillseq_65536x4KiB", {})
-        if world == 1 and a.blocks == 65536 and a.block_size == 4096 and ref:
-            same = comp_sha == ref["comp_sha256"]
-            parity = ("compressed corpus sha256 == reference digest, round trip exact"
-                      if (ok and same) else "MISMATCH")
+        hc = batch.to_host(comps[0])
+        ho = batch.to_host(outs[(a.warmup + a.steps - 1) % a.copies])
+        ok = ok and np.array_equal(corpus.block_digests(ho.buf, ho.off, ho.len),
+                                   corpus.block_digests(c.buf, c.off, c.len))
+        per = corpus.block_digests(hc.buf, hc.off, hc.len)
+        for x in comps[1:]:
+            hx = batch.to_host(x)
+            ok = ok and np.array_equal(corpus.block_digests(hx.buf, hx.off, hx.len), per)
+        oks = [None] * world
+        if dist:
+            dist.all_gather_object(oks, ok)
         else:
-            parity = "round trip exact, status all ok" if ok else "MISMATCH"
+            oks = [ok]
+        allb = gather_digests(dist, rank, world, per, total)
+        if rank == 0:
+            ref = reference_digest(total, a)
+            dd = corpus.digest_of_digests(allb)
+            if not all(oks):
+                parity = "MISMATCH (a rank's round trip or status failed)"
+            elif ref is None:
+                parity = "round trip exact, status all ok (no pinned digest for this stream)"
+            elif dd == ref["comp_dd"]:
+                parity = (f"compressed blocks == reference ({ref['name']} digest of per-block "
+                          f"digests, {world} rank(s) re-interleaved), round trip exact")
+            else:
+                parity = f"MISMATCH against {ref['name']}"
 
     tot_units = raw_bytes * world * a.steps
     value = tot_units / elapsed / 2**30
-    enc_alg = raw_bytes + comp_bytes + 16 * n   # SURVEY §8d per-block bytes x blocks
+    alg = raw_bytes + comp_bytes + 16 * n   # SURVEY §8d per-block bytes x blocks, one launch
     kern = {
-        "encode": {"avg_ms": enc_ms, "alg_bytes": enc_alg,
-                   "achieved_GBps": enc_alg / (enc_ms * 1e-3) / 1e9,
+        "encode": {"avg_ms": enc_ms, "alg_bytes": alg,
+                   "achieved_GBps": alg / (enc_ms * 1e-3) / 1e9,
                    "GiBps_uncompressed": raw_bytes / (enc_ms * 1e-3) / 2**30},
-        "decode": {"avg_ms": dec_ms, "alg_bytes": enc_alg,
-                   "achieved_GBps": enc_alg / (dec_ms * 1e-3) / 1e9,
+        "decode": {"avg_ms": dec_ms, "alg_bytes": alg,
+                   "achieved_GBps": alg / (dec_ms * 1e-3) / 1e9,
                    "GiBps_uncompressed": raw_bytes / (dec_ms * 1e-3) / 2**30},
     }
     dom = "encode" if enc_ms >= dec_ms else "decode"
-    traffic = None
+    traffic, traffic_note = None, "no PMC summary for this workload"
     try:
         tr = json.load(open(a.traffic))
         if tr.get("blocks") == n and dom in tr.get("kernels", {}):
-            traffic = tr["kernels"][dom].get("hbm_bytes_per_launch")
+            if tr.get("sources_sha") == kernel_sources_sha():
+                traffic = tr["kernels"][dom].get("hbm_bytes_per_launch")
+                traffic_note = (f"PMC profile {tr['kernels'][dom].get('profile')} of these "
+                                f"kernel sources ({tr['sources_sha']}), 2*FETCH_SIZE+WRITE_SIZE")
+            else:
+                traffic_note = "PMC summary is from other kernel sources: dropped"
     except (OSError, ValueError):
         pass
     roof = {"bound": "hbm", "kernel": dom, "achieved": kern[dom]["achieved_GBps"],
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": kern[dom]["achieved_GBps"] / HBM_PEAK_GBS, "traffic": traffic}
+            "frac": kern[dom]["achieved_GBps"] / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_note": traffic_note,
+            "alg_bytes_per_block": "raw_len + comp_len + 16 (SURVEY §8d)"}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(c, a)
+        cpu = cpu_baseline(c, a, hc)
 
     if rank == 0:
         line = {
             "metric": baseline["metric"], "value": value, "unit": "GiB/s",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": f"C2: {a.blocks} x {a.block_size // 1024} KiB db_bench "
-                                   f"fillseq blocks per GPU, encode+decode round trip",
-                       "blocks_per_gpu": n, "raw_bytes_per_gpu": raw_bytes,
-                       "comp_bytes_per_gpu": comp_bytes, "ratio": comp_bytes / raw_bytes,
+            "scaling": "weak" if a.blocks else "strong", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": workload_name(total, a, world),
+                       "total_blocks": total, "blocks_rank0": n,
+                       "raw_bytes_rank0": raw_bytes, "comp_bytes_rank0": comp_bytes,
+                       "ratio": comp_bytes / raw_bytes,
                        "partition": "round-robin block g -> rank g % N, no collective",
+                       "process_group": "gloo (barrier, max-over-ranks, parity gather)",
                        "copies_rotated": a.copies},
             "encode_GiBps": raw_bytes * world / (enc_ms * 1e-3) / 2**30,
             "decode_GiBps": raw_bytes * world / (dec_ms * 1e-3) / 2**30,
@@ -211,41 +363,53 @@ def main() -> None:
             "gen_seconds": t_gen,
         }
         print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
 
 
-def cpu_baseline(c, a) -> dict:
-    """Reference snappy.c (oracle/_ref) on a bounded sample of the same blocks."""
+def cpu_threads_share(a) -> int:
+    if a.cpu_threads:
+        return a.cpu_threads
+    share = len(os.sched_getaffinity(0))
+    for var in ("OMP_NUM_THREADS",):      # the GPU box sets the per-GPU CPU share here
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            share = min(share, int(v))
+    return max(1, min(16, share))
+
+
+def cpu_baseline(c, a, gpu_comp) -> dict:
+    """BASELINE.md's CPU-baseline plan: the reference snappy.c (oracle/_ref,
+    compiled unmodified) over the first `--cpu-sample` of this GPU's blocks
+    (all of C2), 1 thread and the host's thread share, outputs pre-faulted,
+    warm-up + median of 5, compressed bytes checked against the GPU's."""
     import oracle
-    codec = oracle.reference()
-    kind = "reference"
+    codec, kind = oracle.reference(), "reference"
     if codec is None:
         codec, kind = oracle.restatement(), "port"
-    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+    nt = cpu_threads_share(a)
     m = min(a.cpu_sample, c.n)
-    buf, off, ln = c.buf, c.off[:m].copy(), c.len[:m].copy()
-    raw = int(ln.sum(dtype=np.uint64))
-    comp = codec.encode_batch(buf, off, ln, threads)            # warm + inputs for decode
-    caps = ln.copy()
-    codec.decode_batch(comp[0], comp[1], comp[2], caps, threads)
-    t_enc, t_dec, reps = [], [], 0
-    t_stop = time.perf_counter() + a.cpu_seconds
-    while reps < 3 or time.perf_counter() < t_stop:
-        t0 = time.perf_counter()
-        codec.encode_batch(buf, off, ln, threads)
-        t1 = time.perf_counter()
-        codec.decode_batch(comp[0], comp[1], comp[2], caps, threads)
-        t2 = time.perf_counter()
-        t_enc.append(t1 - t0)
-        t_dec.append(t2 - t1)
-        reps += 1
-    te, td = float(np.median(t_enc)), float(np.median(t_dec))
-    return {"value": raw / (te + td) / 2**30, "unit": "GiB/s", "cores": threads, "kind": kind,
-            "encode_GiBps": raw / te / 2**30, "decode_GiBps": raw / td / 2**30,
-            "sample": f"first {m} of the GPU's blocks ({raw} B raw), encode+decode pass, "
-                      f"median of {reps} reps, {threads} threads round-robin"}
+    off, ln = c.off[:m].copy(), c.len[:m].copy()
+    plan = oracle.baseline_plan(codec, c.buf, off, ln, sorted({1, nt}), reps=a.cpu_reps)
+    same = None
+    if gpu_comp is not None:
+        from lcdb_amd import corpus
+        co, coo, col = plan["comp"]
+        same = bool(np.array_equal(corpus.block_digests(co, coo, col),
+                                   corpus.block_digests(gpu_comp.buf, gpu_comp.off[:m],
+                                                        gpu_comp.len[:m])))
+    pt = plan["per_threads"]
+    host = oracle.cpu_model()
+    return {"value": pt[nt]["roundtrip_GiBps"], "unit": "GiB/s", "cores": nt,
+            "threads": nt, "kind": kind,
+            "encode_GiBps": pt[nt]["encode_GiBps"], "decode_GiBps": pt[nt]["decode_GiBps"],
+            "single_thread": {k: pt[1][k] for k in ("roundtrip_GiBps", "encode_GiBps",
+                                                     "decode_GiBps")},
+            "cpu_model": host["model"], "physical_cores": host["physical_cores"],
+            "logical_cpus": host["logical_cpus"], "affinity_cpus": host["affinity_cpus"],
+            "same_bytes_as_gpu": same,
+            "sample": f"first {m} of the GPU's blocks ({plan['raw_bytes']} B raw), "
+                      f"encode then decode, warm-up + median of {a.cpu_reps} runs, "
+                      f"1 and {nt} threads (static round-robin), pre-faulted outputs"}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -28,6 +28,18 @@ HIP_HEADERS = ["lgs_device.h", "lgs_launch.h"]
 ARCH = "gfx950"
 
 
+def kernel_sources_sha() -> str:
+    """SHA-256 (16 hex) of the codec's kernel sources: PMC traffic figures in
+    profiles/traffic_latest.json are only reported by bench.py when they were
+    taken from these exact sources."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in sorted(HIP_SOURCES + HIP_HEADERS):
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def _hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):

@@ -136,3 +136,21 @@ def value_ring() -> bytes:
     n = C.c_uint64(0)
     p = _corpus_lib().corpus_ring(C.byref(n))
     return C.string_at(p, n.value)
+
+
+def block_digests(buf: np.ndarray, off: np.ndarray, ln: np.ndarray) -> np.ndarray:
+    """SHA-256 of every block, as an (n, 32) uint8 array (layout-independent)."""
+    n = int(ln.shape[0])
+    out = bytearray(32 * n)
+    mv = memoryview(buf)
+    sha = hashlib.sha256
+    for i, (o, k) in enumerate(zip(off.tolist(), ln.tolist())):
+        out[32 * i:32 * i + 32] = sha(mv[o:o + k]).digest()
+    return np.frombuffer(bytes(out), dtype=np.uint8).reshape(n, 32)
+
+
+def digest_of_digests(per_block: np.ndarray) -> str:
+    """SHA-256 over the per-block SHA-256s in block order: the corpus digest
+    that round-robin shards reassemble without moving the blocks
+    (tests/golden/digests.json "*_dd" fields)."""
+    return hashlib.sha256(np.ascontiguousarray(per_block).tobytes()).hexdigest()

@@ -364,3 +364,68 @@ def time_cpu(codec: Codec, mode: str, buf, off, ln, threads: int, comp=None,
         times.append(time.perf_counter() - t0)
         reps += 1
     return float(np.median(times)), reps
+
+
+def cpu_model() -> dict:
+    """CPU model name and physical-core count of this host (/proc/cpuinfo)."""
+    model, phys = "unknown", set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for line in f.read().splitlines() + [""]:
+                if not line.strip():
+                    if "core id" in cur:
+                        phys.add((cur.get("physical id", "0"), cur["core id"]))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                cur[k.strip()] = v.strip()
+                if k.strip() == "model name" and model == "unknown":
+                    model = v.strip()
+    except OSError:
+        pass
+    return {"model": model, "physical_cores": len(phys) or None,
+            "logical_cpus": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
+
+
+def baseline_plan(codec: Codec, buf, off, ln, thread_counts, reps: int = 5) -> dict:
+    """BASELINE.md "CPU-baseline plan": the codec over the same blocks the GPU
+    timed, once per thread count (static round-robin partition, cpu_batch.c),
+    outputs in pre-faulted buffers reused across runs, one untimed warm-up,
+    then the median of `reps` timed runs, encode and decode separately.
+    Returns per-thread-count GiB/s plus the compressed output (for the
+    byte-for-byte check against the GPU's)."""
+    n = int(ln.shape[0])
+    raw = int(ln.sum(dtype=np.uint64))
+    bounds = (ln.astype(np.uint64) * 7 // 6 + 48) // 16 * 16
+    ooff = np.zeros(n, dtype=np.uint64)
+    if n:
+        ooff[1:] = np.cumsum(bounds[:-1])
+    comp = np.ones(int(bounds.sum()) + 16, dtype=np.uint8)       # ones: pre-faulted
+    olen = np.zeros(n, dtype=np.uint32)
+    caps64 = (ln.astype(np.uint64) + 15) // 16 * 16
+    doff = np.zeros(n, dtype=np.uint64)
+    if n:
+        doff[1:] = np.cumsum(caps64[:-1])
+    dec = np.ones(int(caps64.sum()) + 16, dtype=np.uint8)
+    st = np.zeros(n, dtype=np.uint8)
+    res = {}
+    for t in thread_counts:
+        te, td = [], []
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            codec._batch(0, codec.f_encode, t, buf, off, ln, comp, ooff, olen, None)
+            t1 = time.perf_counter()
+            codec._batch(1, codec.f_decode, t, comp, ooff, olen, dec, doff, None, st)
+            t2 = time.perf_counter()
+            if r:                      # run 0 is the warm-up
+                te.append(t1 - t0)
+                td.append(t2 - t1)
+        if not bool((st == 1).all()):
+            raise RuntimeError("CPU baseline: reference decode rejected its own output")
+        e, d = float(np.median(te)), float(np.median(td))
+        res[t] = {"encode_GiBps": raw / e / 2**30, "decode_GiBps": raw / d / 2**30,
+                  "roundtrip_GiBps": raw / (e + d) / 2**30,
+                  "encode_s_median": e, "decode_s_median": d}
+    return {"per_threads": res, "raw_bytes": raw, "comp": (comp, ooff, olen)}

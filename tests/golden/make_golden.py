@@ -226,29 +226,49 @@ def main() -> None:
 
     write(VECTORS, vecs)
 
-    # -- digests of the BASELINE.json corpora (reference outputs) --
-    def digest(c: corpus.Corpus, threads: int = 8) -> dict:
-        out, ooff, olen = ref.encode_batch(c.buf, c.off, c.len, threads=threads)
-        h = hashlib.sha256()
-        for o, k in zip(ooff, olen):
-            h.update(memoryview(out[int(o):int(o) + int(k)]))
-        return {"blocks": c.n, "raw_bytes": c.raw_bytes, "raw_sha256": c.sha256(),
-                "comp_bytes": int(olen.sum(dtype=np.uint64)), "comp_sha256": h.hexdigest()}
+    make_digests(ref)
+    print(f"{len(vecs)} vectors, {os.path.getsize(VECTORS)} bytes")
 
+
+def make_digests(ref) -> None:
+    """Digests of the BASELINE.json corpora (reference outputs).
+
+    ``*_sha256``: SHA-256 of the concatenated blocks; ``*_dd``: SHA-256 of the
+    concatenated per-block SHA-256s (lcdb_amd.corpus.digest_of_digests), which
+    round-robin shards reassemble without moving blocks (bench.py at N > 1).
+    C4 (1 048 576 blocks, BASELINE.json configs[3]) is pinned by its _dd
+    digests only."""
+    def digest(c: corpus.Corpus, threads: int = 8, concat: bool = True) -> dict:
+        out, ooff, olen = ref.encode_batch(c.buf, c.off, c.len, threads=threads)
+        d = {"blocks": c.n, "raw_bytes": c.raw_bytes,
+             "comp_bytes": int(olen.sum(dtype=np.uint64)),
+             "raw_dd": corpus.digest_of_digests(corpus.block_digests(c.buf, c.off, c.len)),
+             "comp_dd": corpus.digest_of_digests(corpus.block_digests(out, ooff, olen))}
+        if concat:
+            h = hashlib.sha256()
+            for o, k in zip(ooff, olen):
+                h.update(memoryview(out[int(o):int(o) + int(k)]))
+            d.update(raw_sha256=c.sha256(), comp_sha256=h.hexdigest())
+        return d
+
+    ramp = ref.encode(bytes(i & 255 for i in range(1 << 20)))
     digs = {
         "C1_fillseq_1024x4KiB": digest(corpus.fillseq(1024)),
         "C2_fillseq_65536x4KiB": digest(corpus.fillseq(65536)),
         "C3_mixed": digest(corpus.mixed()),
-        "ramp_1MiB": {"raw_bytes": 1 << 20, "comp_bytes": len(ref.encode(bytes(i & 255 for i in range(1 << 20)))),
-                      "comp_sha256": hashlib.sha256(ref.encode(bytes(i & 255 for i in range(1 << 20)))).hexdigest()},
+        "C4_fillseq_1048576x4KiB": digest(corpus.fillseq(1048576), concat=False),
+        "ramp_1MiB": {"raw_bytes": 1 << 20, "comp_bytes": len(ramp),
+                      "comp_sha256": hashlib.sha256(ramp).hexdigest()},
         "_generator": "tests/golden/make_golden.py with oracle/_ref/libref_snappy.so "
                       "(lcdb src/util/snappy.c compiled unmodified)",
     }
     with open(DIGESTS, "w") as f:
         json.dump(digs, f, indent=2, sort_keys=True)
-    print(f"{len(vecs)} vectors, {os.path.getsize(VECTORS)} bytes; digests: "
-          + ", ".join(k for k in digs if not k.startswith("_")))
-
+    print("digests: " + ", ".join(k for k in digs if not k.startswith("_")))
 
 if __name__ == "__main__":
-    main()
+    if "--digests-only" in sys.argv:
+        import oracle
+        make_digests(oracle.reference())
+    else:
+        main()

@@ -6,8 +6,11 @@ reduction must return the max over ranks."""
 from __future__ import annotations
 
 import hashlib
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import pytest
 import torch.distributed as dist
@@ -17,6 +20,7 @@ import oracle
 from lcdb_amd import shard
 
 WORLD = 2
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
 PER_RANK = 512          # 2 x 512 = the 1024 blocks of digest C1
 
 
@@ -82,3 +86,58 @@ def test_shards_are_slices_of_one_stream(world):
         s = shard.fillseq_shard(8, r, world)
         for i in range(8):
             assert s.block(i) == full.block(shard.global_index(i, r, world))
+
+
+def _bench(*args: str, env=None) -> subprocess.CompletedProcess:
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True,
+                          timeout=600, env=e)
+
+
+def _last_json(out: str) -> dict:
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_launcher_ws2_reassembles_c1(digests):
+    """bench.py's own launcher (--gpus 2, no WORLD_SIZE) starts 2 gloo ranks;
+    their round-robin shards, re-interleaved by the parity gather, are the
+    C1 stream (per-block digests in global order == the pinned raw_dd)."""
+    r = _bench("--gpus", "2", "--plan-only", "--total-blocks", "1024")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["blocks_rank0"] == 512
+    assert line["raw_dd"] == digests["C1_fillseq_1024x4KiB"]["raw_dd"]
+    assert line["max_over_ranks"] == 2.0
+
+
+@pytest.mark.slow
+def test_bench_launcher_c4_default(digests):
+    """At N > 1 the default workload is C4: 1 048 576 blocks dealt g -> g % N."""
+    r = _bench("--gpus", "2", "--plan-only")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["workload"].startswith("C4:")
+    assert line["total_blocks"] == 1048576 and line["blocks_rank0"] == 524288
+    assert line["raw_dd"] == digests["C4_fillseq_1048576x4KiB"]["raw_dd"]
+
+
+def test_bench_rejects_world_mismatch():
+    r = _bench("--gpus", "4", "--plan-only", "--total-blocks", "64",
+               env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def test_oracle_shards_reassemble_to_reference_dd(digests):
+    """comp_dd (digest of per-block digests) of C1 from ws=3 round-robin
+    shards encoded by the reference codec equals the pinned comp_dd."""
+    from lcdb_amd import corpus
+    codec = oracle.best()
+    per = []
+    for r in range(3):
+        c = shard.fillseq_total(1024, r, 3)
+        out, ooff, olen = codec.encode_batch(c.buf, c.off, c.len, 2)
+        per.append(corpus.block_digests(out, ooff, olen))
+    allb = shard.interleave(per, 1024)
+    assert corpus.digest_of_digests(allb) == digests["C1_fillseq_1024x4KiB"]["comp_dd"]

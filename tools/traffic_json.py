@@ -45,6 +45,9 @@ def main() -> None:
             "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950, MI355X_MICROARCH.md HBM)",
         }
     cur["blocks"] = 65536
+    sys.path.insert(0, ROOT)
+    from lcdb_amd.build import kernel_sources_sha
+    cur["sources_sha"] = kernel_sources_sha()   # bench.py drops traffic on a mismatch
     json.dump(cur, open(OUT, "w"), indent=1, sort_keys=True)
     print(json.dumps(cur, indent=1))
 
