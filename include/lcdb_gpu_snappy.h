@@ -20,14 +20,25 @@
  *
  *    Callers: src/table/table_builder.c:182,187 (encode) and
  *    src/table/format.c:237,247 (decode); both pass pageable host buffers.
- *    encode/decode stage through pinned memory on a per-thread HIP stream;
- *    both are thread-safe.  Compressed bytes are identical to the reference
- *    encoder's and decode accepts/rejects exactly what the reference does.
- *    The *_size functions are header arithmetic (a bound, a varint32 read)
- *    and run on the host.  Encode has no error path in lcdb, so a HIP
- *    failure inside ldb_snappy_encode prints a diagnostic and aborts (there
- *    is no silent CPU fallback).  On a decode failure the contents of zp are
- *    unspecified, as in the reference.
+ *    Both are thread-safe.  A call leases one of a bounded pool of staging
+ *    slots (per device: at most LGS_DROPIN_SLOTS = 8 slots of LGS_DROPIN_MB =
+ *    4 MiB pinned + 4 MiB device memory, created on first use; a caller waits
+ *    while all are leased), so the drop-in's memory is bounded whatever the
+ *    input: encode runs any input through its slot in passes of whole 64 KiB
+ *    chunks (independent, snappy.c:370-381); decode rejects on the host every
+ *    stream whose size header its length cannot satisfy (exactly the
+ *    reference's result, no device work), and decodes a block larger than a
+ *    slot in device memory taken for that call only.
+ *    Compressed bytes are identical to the reference encoder's and decode
+ *    accepts/rejects exactly what the reference does.  The *_size functions
+ *    are header arithmetic (a bound, a varint32 read) and run on the host.
+ *    Errors: lcdb's encode path has no error return (table_builder.c:182-
+ *    188), so ldb_snappy_encode aborts with a diagnostic only when the device
+ *    fails (or no slot at all can be created); ldb_snappy_decode returns 0
+ *    (LDB_CORRUPTION at format.c:247-251) with a diagnostic when device
+ *    memory for an over-slot block runs out, and aborts only when the device
+ *    fails.  There is no CPU fallback.  On a decode failure the contents of
+ *    zp are unspecified, as in the reference.
  *
  * 2. The batched API (lgs_*), new: tens of thousands of independent blocks
  *    per launch.  Blocks are addressed by byte offsets into one base buffer.
@@ -91,9 +102,10 @@ int lgs_encode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
    extend at least 16 bytes beyond the last block.
    Both _dev calls: a batch of >= 512 blocks whose largest block is over
    4 608 bytes is sorted into size classes on the device first, with up to
-   16 bytes per block of stream-ordered scratch from the device's default
-   memory pool (hipMallocAsync, freed on `stream`); LGS_ENOMEM-class HIP
-   errors are possible there.  LGS_NO_SPLIT=1 turns this off. */
+   16 bytes per block of stream-ordered scratch from a private memory pool
+   of the device (hipMallocFromPoolAsync, freed on `stream`; the process's
+   default pool is not touched); LGS_ENOMEM-class HIP errors are possible
+   there.  lgs_set_option("split", "0") turns this off. */
 int lgs_decode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
                          const uint32_t *d_in_len, uint8_t *d_out,
                          const uint64_t *d_out_off, const uint32_t *d_out_cap,
@@ -101,8 +113,10 @@ int lgs_decode_batch_dev(const uint8_t *d_in, const uint64_t *d_in_off,
                          uint32_t max_out_cap, void *stream);
 
 /* Host-buffer variants: same layout with host pointers (pageable is fine).
-   Data moves through pinned staging with hipMemcpyAsync on a per-thread
-   stream; the call returns when the results are in the caller's buffers. */
+   Data moves through pinned staging with hipMemcpyAsync on a pooled
+   context's stream (contexts are leased per call, never tied to a thread;
+   their arenas grow to the largest batch served); the call returns when the
+   results are in the caller's buffers. */
 int lgs_encode_batch_host(const uint8_t *in, const uint64_t *in_off,
                           const uint32_t *in_len, uint8_t *out,
                           const uint64_t *out_off, uint32_t *out_len,
@@ -285,6 +299,19 @@ int lgs_filter_block_match_host(const uint8_t *block, size_t block_len,
                                 int internal_keys, uint8_t *match);
 
 /* Devices and diagnostics. */
+/* The drop-in's current footprint: pinned and device bytes held by its
+   staging slots, the number of slots created (all devices) and the bytes of
+   one slot's arena.  The totals never exceed slots * slot_bytes. */
+int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
+                         size_t *slot_bytes);
+
+/* Process-wide kernel choices (A/B and tests; the defaults pick by batch):
+     "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
+     "split":   "1" | "0"  (size-class split of mixed batches, see above)
+   Initial values: LGS_DECODE_KERNEL, LGS_NO_SPLIT=1, read once at load.
+   LGS_EINVAL for an unknown name or value. */
+int lgs_set_option(const char *name, const char *value);
+
 int lgs_device_count(void);
 int lgs_set_device(int device);  /* device used by the calling thread */
 const char *lgs_last_error(void);

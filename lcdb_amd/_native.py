@@ -62,6 +62,9 @@ _SIGS = {
                                              C.c_int, _vp, _vp]),
     "lgs_filter_block_match_host": (C.c_int, [_vp, C.c_size_t, _vp, _vp, _vp, _vp, C.c_uint32,
                                               C.c_int, _vp]),
+    "lgs_dropin_footprint": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
+                                       C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]),
+    "lgs_set_option": (C.c_int, [C.c_char_p, C.c_char_p]),
     "lgs_device_count": (C.c_int, []),
     "lgs_set_device": (C.c_int, [C.c_int]),
     "lgs_last_error": (C.c_char_p, []),
@@ -100,6 +103,19 @@ def lib() -> C.CDLL:
 
 class LgsError(RuntimeError):
     pass
+
+
+def set_option(name: str, value: str) -> None:
+    """lgs_set_option: process-wide kernel choice ("decoder", "split")."""
+    check(lib().lgs_set_option(name.encode(), value.encode()), f"lgs_set_option({name})")
+
+
+def dropin_footprint() -> dict:
+    """Bytes the drop-in's staging slots hold (lgs_dropin_footprint)."""
+    p, d, n, cap = C.c_size_t(0), C.c_size_t(0), C.c_uint32(0), C.c_size_t(0)
+    check(lib().lgs_dropin_footprint(C.byref(p), C.byref(d), C.byref(n), C.byref(cap)),
+          "lgs_dropin_footprint")
+    return {"pinned": p.value, "device": d.value, "slots": n.value, "slot_bytes": cap.value}
 
 
 def check(rc: int, what: str) -> None:

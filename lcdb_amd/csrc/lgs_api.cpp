@@ -2,15 +2,26 @@
 // (declarations, and the reference interfaces they replace:
 // include/lcdb_gpu_snappy.h).
 //
-// Per calling thread: one non-blocking HIP stream on the selected device, a
-// growable device arena and a growable pinned host arena.  lcdb enters the
+// HIP resources live in contexts (a non-blocking stream on one device plus a
+// device arena and a pinned host arena) that are pooled per device and
+// leased for the length of one call, never tied to a thread: lcdb enters the
 // codec concurrently from user threads (reads) and its compaction thread
-// (writes) (db_impl.c:1614-1652), so nothing here is shared between threads
-// except the HIP runtime itself.
+// (writes) (db_impl.c:1614-1652), and a host may create and join threads
+// freely without leaking pinned memory.  Two pools:
+//   * the drop-in's (ldb_snappy_*): at most LGS_DROPIN_SLOTS contexts per
+//     device (default 8), each with fixed arenas of LGS_DROPIN_MB (default 4)
+//     MiB that never grow -- any input size is handled in bounded passes;
+//   * the batched host API's (lgs_*_host): arenas grow to the largest batch
+//     a context has served, at most 16 contexts per device.
+// A caller waits when its device's contexts are all leased.
 //
 // No compression or decompression happens on the host.  The host only moves
 // bytes (pageable <-> pinned <-> device), computes the size bound
-// (snappy.c:347-362) and reads the varint32 size header (snappy.c:386-399).
+// (snappy.c:347-362) and reads the varint32 size header (snappy.c:386-399),
+// and rejects on the host the streams whose header the stream's length
+// cannot satisfy (an arithmetic bound, below) -- the reference rejects them
+// too, so the result is the same without a device round trip.
+
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -145,7 +156,6 @@ void par_for(uint32_t n, size_t bytes, const F& f) {
 
 struct Ctx {
   int device = -1;          // device this context's resources live on
-  int want_device = -1;     // lgs_set_device() choice (-1: current device)
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;   // the chunk pipeline's second stream (lazily)
   hipEvent_t done[2] = {nullptr, nullptr};
@@ -153,36 +163,195 @@ struct Ctx {
   size_t d_cap = 0;
   uint8_t* h_buf = nullptr; // pinned
   size_t h_cap = 0;
+  bool fixed = false;       // a drop-in slot: arenas never grow
 };
 
-// Deliberately never destroyed: freeing HIP resources from thread-exit
-// destructors can run after the runtime is torn down at process exit.
-thread_local Ctx t_ctx;
+// lgs_set_device() choice of the calling thread (-1: its current device).
+thread_local int t_want_device = -1;
 
-int ctx_ready(Ctx& c) {
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
-    return fail(LGS_ENODEV, "no HIP device visible");
-  int dev = c.want_device;
-  if (dev < 0) {
-    LGS_HIP(hipGetDevice(&dev));
+int visible_devices() {
+  static const int n = [] {
+    int c = 0;
+    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+  }();
+  return n;
+}
+
+// The device a call from this thread runs on (made current for the thread).
+int call_device(int* dev) {
+  const int count = visible_devices();
+  if (count <= 0) return fail(LGS_ENODEV, "no HIP device visible");
+  if (t_want_device < 0) {
+    LGS_HIP(hipGetDevice(dev));
   } else {
-    if (dev >= count) return fail(LGS_ENODEV, "device %d not present (%d visible)", dev, count);
-    LGS_HIP(hipSetDevice(dev));
+    if (t_want_device >= count)
+      return fail(LGS_ENODEV, "device %d not present (%d visible)", t_want_device, count);
+    *dev = t_want_device;
+    LGS_HIP(hipSetDevice(*dev));
   }
-  if (c.device != dev || c.stream == nullptr) {
-    // A thread that switches devices abandons the previous device's buffers
-    // (they are not freed from the wrong device).
-    const int keep = c.want_device;
-    c = Ctx{};
-    c.want_device = keep;
-    c.device = dev;
-    LGS_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-  }
+  if (*dev < 0 || *dev >= 64) return fail(LGS_ENODEV, "device %d out of range", *dev);
   return LGS_OK;
 }
 
+size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
+  const char* e = getenv(name);
+  long v = e ? atol(e) : 0;
+  size_t r = v > 0 ? (size_t)v : dflt;
+  return r < lo ? lo : (r > hi ? hi : r);
+}
+
+// Drop-in slot arenas (pinned and device, each): LGS_DROPIN_MB MiB, at least
+// 1 (one 64 KiB chunk's input and bound-sized output fit with room to spare).
+size_t dropin_cap() {
+  static const size_t v = env_size("LGS_DROPIN_MB", 4, 1, 1024) << 20;
+  return v;
+}
+unsigned dropin_max_slots() {
+  static const unsigned v = (unsigned)env_size("LGS_DROPIN_SLOTS", 8, 1, 256);
+  return v;
+}
+
+// Contexts of one kind, per device.  Created on demand up to `max` per
+// device; HIP resources are never freed (freeing from static destructors can
+// run after the runtime is torn down at process exit).
+class CtxPool {
+ public:
+  CtxPool(unsigned max, size_t fixed_cap) : max_(max), fixed_cap_(fixed_cap) {}
+
+  // Lease a context on the calling thread's device; waits while all of that
+  // device's contexts are leased.
+  int acquire(Ctx** out) {
+    int dev = -1;
+    LGS_TRY(call_device(&dev));
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      std::vector<Ctx*>& fl = free_[dev];
+      if (!fl.empty()) {
+        *out = fl.back();
+        fl.pop_back();
+        return LGS_OK;
+      }
+      if (live_[dev] < max_) break;
+      cv_.wait(lk);
+    }
+    ++live_[dev];
+    lk.unlock();
+    Ctx* c = new Ctx;
+    c->device = dev;
+    const int rc = create(c);
+    if (rc != LGS_OK) {
+      destroy_partial(c);
+      lk.lock();
+      --live_[dev];
+      const bool others = live_[dev] > 0;
+      lk.unlock();
+      cv_.notify_all();
+      // Out of pinned or device memory while other contexts exist: wait for
+      // one of them instead of failing the call.
+      if (rc == LGS_ENOMEM && others) return acquire_existing(dev, out);
+      return rc;
+    }
+    *out = c;
+    return LGS_OK;
+  }
+
+  void release(Ctx* c) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      free_[c->device].push_back(c);
+    }
+    cv_.notify_one();
+  }
+
+  // Bytes of pinned / device memory held by this pool's contexts.
+  void footprint(size_t* pinned, size_t* device, unsigned* count) {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t p = 0, d = 0;
+    unsigned n = 0;
+    for (const Ctx* c : all_) {
+      p += c->h_cap;
+      d += c->d_cap;
+      ++n;
+    }
+    *pinned = p;
+    *device = d;
+    *count = n;
+  }
+
+  size_t fixed_cap() const { return fixed_cap_; }
+
+ private:
+  int create(Ctx* c) {
+    LGS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (fixed_cap_) {
+      c->fixed = true;
+      if (hipMalloc(&c->d_buf, fixed_cap_) != hipSuccess)
+        return fail(LGS_ENOMEM, "hipMalloc(%zu) failed", fixed_cap_);
+      c->d_cap = fixed_cap_;
+      if (hipHostMalloc(&c->h_buf, fixed_cap_, hipHostMallocDefault) != hipSuccess)
+        return fail(LGS_ENOMEM, "hipHostMalloc(%zu) failed", fixed_cap_);
+      c->h_cap = fixed_cap_;
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    all_.push_back(c);
+    return LGS_OK;
+  }
+  static void destroy_partial(Ctx* c) {
+    if (c->h_buf) (void)hipHostFree(c->h_buf);
+    if (c->d_buf) (void)hipFree(c->d_buf);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+  }
+  int acquire_existing(int dev, Ctx** out) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return !free_[dev].empty(); });
+    *out = free_[dev].back();
+    free_[dev].pop_back();
+    return LGS_OK;
+  }
+
+  const unsigned max_;
+  const size_t fixed_cap_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Ctx*> free_[64];
+  unsigned live_[64] = {};
+  std::vector<Ctx*> all_;
+};
+
+CtxPool& dropin_pool() {
+  static CtxPool* p = new CtxPool(dropin_max_slots(), dropin_cap());
+  return *p;
+}
+CtxPool& batch_pool() {
+  static CtxPool* p = new CtxPool(16, 0);
+  return *p;
+}
+
+// One context, leased for the length of a call.
+class Lease {
+ public:
+  explicit Lease(CtxPool& p) : pool_(p) {}
+  ~Lease() {
+    if (c_) pool_.release(c_);
+  }
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+  int acquire() { return pool_.acquire(&c_); }
+  Ctx& ctx() { return *c_; }
+
+ private:
+  CtxPool& pool_;
+  Ctx* c_ = nullptr;
+};
+
 int ctx_reserve(Ctx& c, size_t dev_bytes, size_t pin_bytes) {
+  if (c.fixed) {
+    if (dev_bytes > c.d_cap || pin_bytes > c.h_cap)
+      return fail(LGS_EINTERNAL, "drop-in slot of %zu bytes, %zu needed", c.d_cap,
+                  dev_bytes > pin_bytes ? dev_bytes : pin_bytes);
+    return LGS_OK;
+  }
   if (dev_bytes > c.d_cap) {
     if (c.d_buf) LGS_HIP(hipFree(c.d_buf));
     c.d_buf = nullptr;
@@ -277,7 +446,8 @@ struct Layout {
   }
 };
 
-// coding.h:169-204 on the host, for the size header only.
+// coding.h:169-204 on the host, for the size header only.  Returns the
+// header's length in bytes (1-5), 0 if there is no valid header.
 int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
   uint32_t acc = 0;
   unsigned sh = 0;
@@ -285,7 +455,7 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
     const uint32_t b = p[i];
     if ((b & 0x80u) == 0) {
       *v = acc | (b << sh);
-      return 1;
+      return (int)i + 1;
     }
     acc |= (b & 0x7fu) << sh;
   }
@@ -298,103 +468,132 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
   abort();
 }
 
-// Encode one host block of any length on the GPU.
+// ---- the drop-in (ldb_snappy_encode / ldb_snappy_decode) ----
+//
+// Single blocks from lcdb's table builder and block reader.  Every call
+// leases a drop-in slot (fixed arenas of dropin_cap() bytes), so a call
+// never allocates: an input of any size goes through the slot in passes of
+// whole 64 KiB chunks, which are independent (snappy.c:370-381), and the
+// chunks' encodings are concatenated on the host as they come back.  One
+// pass = one upload, one kernel, one download, one synchronisation.
+
+// Device bytes one 64 KiB-or-less chunk takes in a pass.
+constexpr size_t kChunkIn = kChunk + 16;                         // its input
+size_t chunk_out(uint32_t len) { return align_up(bound_of(len) + 8, 16); }
+
 int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
   if (xn > 0x7fffffffu) return fail(LGS_EINVAL, "input of %zu bytes too large", xn);
+  Lease lease(dropin_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   const uint32_t n = (uint32_t)xn;
-  // snappy.c:370-381: full 64 KiB chunks, then the remainder (if any).
+  // snappy.c:370-381: full 64 KiB chunks, then the remainder (if any);
+  // a zero-length input is one empty item (just the varint header).
   const uint32_t nit = n <= kChunk ? 1u : (n + kChunk - 1) / kChunk;
-  const bool single = nit == 1;
-
-  size_t scratch_bytes = 0;
-  for (uint32_t j = 0; j < nit; ++j) {
-    const uint32_t len = j + 1 < nit ? kChunk : n - j * kChunk;
-    scratch_bytes += align_up(bound_of(len) + 8, 16);
-  }
-  const size_t final_bytes = bound_of(n);
-
-  Layout L;  // upload | download | device-only
-  const size_t o_in = L.take(n + 16);
-  const size_t o_ioff = L.take(8 * (size_t)nit);
-  const size_t o_ilen = L.take(4 * (size_t)nit);
-  const size_t o_ooff = L.take(8 * (size_t)nit);
-  const size_t o_hdr = L.take(4 * (size_t)nit);
-  const size_t up_end = L.at;
-  const size_t o_olen = L.take(4 * (size_t)nit);
-  const size_t o_dst_off = L.take(8 * (size_t)nit);
-  const size_t o_final = L.take(final_bytes + 16);
-  const size_t down_end = L.at;
-  const size_t o_scratch = L.take(single ? 0 : scratch_bytes);
-  LGS_TRY(ctx_reserve(c, L.at, down_end));
-
-  uint8_t* h = c.h_buf;
-  uint8_t* d = c.d_buf;
-  memcpy(h + o_in, xp, n);
-  uint64_t* ioff = (uint64_t*)(h + o_ioff);
-  uint32_t* ilen = (uint32_t*)(h + o_ilen);
-  uint64_t* ooff = (uint64_t*)(h + o_ooff);
-  uint32_t* hdr = (uint32_t*)(h + o_hdr);
-  size_t sat = 0;
-  for (uint32_t j = 0; j < nit; ++j) {
-    const uint32_t len = j + 1 < nit ? kChunk : n - j * kChunk;
-    ioff[j] = o_in + (size_t)j * kChunk;
-    ilen[j] = len;
-    hdr[j] = j == 0 ? n : 0xffffffffu;
-    ooff[j] = single ? o_final : o_scratch + sat;
-    sat += align_up(bound_of(len) + 8, 16);
-  }
-  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
-
-  EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
-               (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen),
-               (const uint32_t*)(d + o_hdr), nullptr, nit, nullptr};
-  LGS_HIP(launch_encode(a, single ? n : kChunk, c.stream));
-
-  uint32_t* olen = (uint32_t*)(h + o_olen);
+  // Chunks per pass: per chunk its input, its output slot and 32 bytes of
+  // per-item arrays, plus 7 x 256 of alignment slack.
+  const size_t per = kChunkIn + chunk_out(kChunk) + 32 + 64;
+  const uint32_t kmax = (uint32_t)((c.h_cap - 8 * 256) / per);
+  if (kmax == 0) return fail(LGS_EINTERNAL, "drop-in slot of %zu bytes too small", c.h_cap);
+  uint8_t* const h = c.h_buf;
+  uint8_t* const d = c.d_buf;
   size_t total = 0;
-  if (single) {
+  for (uint32_t j0 = 0; j0 < nit; j0 += kmax) {
+    const uint32_t k = nit - j0 < kmax ? nit - j0 : kmax;
+    const size_t at = (size_t)j0 * kChunk;                      // input offset of the pass
+    const size_t in_bytes = n - at < (size_t)k * kChunk ? n - at : (size_t)k * kChunk;
+    Layout L;                                                    // upload | download
+    const size_t o_in = L.take(in_bytes + 16);
+    const size_t o_ioff = L.take(8 * (size_t)k);
+    const size_t o_ilen = L.take(4 * (size_t)k);
+    const size_t o_ooff = L.take(8 * (size_t)k);
+    const size_t o_hdr = L.take(4 * (size_t)k);
+    const size_t up_end = L.at;
+    const size_t o_olen = L.take(4 * (size_t)k);
+    size_t out_bytes = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+      const size_t off = (size_t)j * kChunk;
+      const uint32_t len = (uint32_t)(in_bytes - off < kChunk ? in_bytes - off : kChunk);
+      out_bytes += chunk_out(len);
+    }
+    const size_t o_out = L.take(out_bytes);
+    const size_t down_end = L.at;
+    LGS_TRY(ctx_reserve(c, down_end, down_end));
+
+    memcpy(h + o_in, xp + at, in_bytes);
+    uint64_t* ioff = (uint64_t*)(h + o_ioff);
+    uint32_t* ilen = (uint32_t*)(h + o_ilen);
+    uint64_t* ooff = (uint64_t*)(h + o_ooff);
+    uint32_t* hdr = (uint32_t*)(h + o_hdr);
+    size_t oa = o_out;
+    for (uint32_t j = 0; j < k; ++j) {
+      const size_t off = (size_t)j * kChunk;
+      ilen[j] = (uint32_t)(in_bytes - off < kChunk ? in_bytes - off : kChunk);
+      ioff[j] = o_in + off;
+      ooff[j] = oa;
+      oa += chunk_out(ilen[j]);
+      hdr[j] = j0 + j == 0 ? n : 0xffffffffu;                    // snappy.c:368
+    }
+    LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+    EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
+                 (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen),
+                 (const uint32_t*)(d + o_hdr), nullptr, k, nullptr};
+    LGS_HIP(launch_encode(a, k == 1 ? ilen[0] : kChunk, c.stream));
     LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, down_end - o_olen, hipMemcpyDeviceToHost,
                            c.stream));
     LGS_HIP(hipStreamSynchronize(c.stream));
-    total = olen[0];
-  } else {
-    // Chunk outputs are concatenated on the device once their lengths are
-    // known (one small round trip for the lengths).
-    LGS_HIP(hipMemcpyAsync(olen, d + o_olen, 4 * (size_t)nit, hipMemcpyDeviceToHost, c.stream));
-    LGS_HIP(hipStreamSynchronize(c.stream));
-    uint64_t* doff = (uint64_t*)(h + o_dst_off);
-    for (uint32_t j = 0; j < nit; ++j) {
-      doff[j] = o_final + total;
+    const uint32_t* olen = (const uint32_t*)(h + o_olen);
+    for (uint32_t j = 0; j < k; ++j) {
+      if (olen[j] > chunk_out(ilen[j]))
+        return fail(LGS_EINTERNAL, "encoded chunk of %u bytes exceeds its bound", olen[j]);
+      memcpy(zp + total, h + ooff[j], olen[j]);
       total += olen[j];
     }
-    LGS_HIP(hipMemcpyAsync(d + o_dst_off, doff, 8 * (size_t)nit, hipMemcpyHostToDevice, c.stream));
-    LGS_HIP(launch_concat(d, (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_olen), d,
-                          (const uint64_t*)(d + o_dst_off), nit, c.stream));
-    LGS_HIP(hipMemcpyAsync(h + o_final, d + o_final, total, hipMemcpyDeviceToHost, c.stream));
-    LGS_HIP(hipStreamSynchronize(c.stream));
   }
-  if (total > final_bytes) return fail(LGS_EHIP, "encoded length %zu exceeds bound", total);
-  memcpy(zp, h + o_final, total);
+  if (total > bound_of(n)) return fail(LGS_EINTERNAL, "encoded length %zu exceeds bound", total);
   *written = total;
   return LGS_OK;
 }
 
+// Host-side reference rejects, from the header and the stream length only
+// (snappy.c:201-341): with m stream bytes after a header of `want`,
+//   * want == 0: the reference accepts exactly when m == 0 (every tag either
+//     produces >= 1 byte, failing len > zn, or is a copy failing :323);
+//   * a COPY2 tag (3 bytes) yields at most 64 bytes, every other tag less
+//     per byte, so 3 * want > 64 * m can never reach zn == 0 (:337);
+//   * a tag consumes at most 6 bytes per byte it yields (a literal of one
+//     byte with a 4-byte length: 1 + 4 + 1), so m > 6 * want must run out
+//     of output first (:263, :323).
+// Returns 1 (accept), 0 (reject) or -1 (the device decides).
+int host_verdict(uint32_t want, size_t m) {
+  if (want == 0) return m == 0 ? 1 : 0;
+  if (3 * (uint64_t)want > 64 * (uint64_t)m) return 0;
+  if ((uint64_t)m > 6 * (uint64_t)want) return 0;
+  return -1;
+}
+
 // Decode one host block on the GPU.  *ok = reference decode result.
 int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
+  *ok = 0;
   uint32_t want = 0;
-  if (!read_varint32(&want, xp, xn) || want > 0x7fffffffu) {  // snappy.c:405-409
-    *ok = 0;
+  const int hl = read_varint32(&want, xp, xn);
+  if (hl == 0 || want > 0x7fffffffu) return LGS_OK;            // snappy.c:405-409
+  const int hv = host_verdict(want, xn - (size_t)hl);
+  if (hv >= 0) {
+    *ok = hv;
     return LGS_OK;
   }
-  if (xn > 0xffffffffu) return fail(LGS_EINVAL, "input of %zu bytes too large", xn);
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  // (Blocks are addressed with 32-bit lengths on the device; lcdb's blocks
+  // are far smaller.)
+  if (xn > 0xffffffffu) return fail(LGS_ENOMEM, "a %zu-byte stream is too large", xn);
   const uint32_t n = (uint32_t)xn;
+  Lease lease(dropin_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
+  uint8_t* const h = c.h_buf;
 
   Layout L;
-  const size_t o_in = L.take(n + 16);
+  const size_t o_in = L.take((size_t)n + 16);
   const size_t o_ioff = L.take(8);
   const size_t o_ilen = L.take(4);
   const size_t o_ooff = L.take(8);
@@ -404,31 +603,87 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   const size_t o_olen = L.take(4);
   const size_t o_out = L.take((size_t)want + 16);
   const size_t down_end = L.at;
-  LGS_TRY(ctx_reserve(c, down_end, down_end));
-
-  uint8_t* h = c.h_buf;
-  uint8_t* d = c.d_buf;
-  memcpy(h + o_in, xp, n);
-  *(uint64_t*)(h + o_ioff) = o_in;
-  *(uint32_t*)(h + o_ilen) = n;
-  *(uint64_t*)(h + o_ooff) = o_out;
-  *(uint32_t*)(h + o_ocap) = want;
-  LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
-  DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
-               (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
-               (uint32_t*)(d + o_olen), d + o_st, nullptr, 1, nullptr};
+  if (down_end <= c.h_cap) {
+    // In the slot: one upload, one kernel, one download (status, length and
+    // the bounded output together), one synchronisation.
+    uint8_t* const d = c.d_buf;
+    memcpy(h + o_in, xp, n);
+    *(uint64_t*)(h + o_ioff) = o_in;
+    *(uint32_t*)(h + o_ilen) = n;
+    *(uint64_t*)(h + o_ooff) = o_out;
+    *(uint32_t*)(h + o_ocap) = want;
+    LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
+    DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
+                 (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
+                 (uint32_t*)(d + o_olen), d + o_st, nullptr, 1, nullptr};
+    LGS_HIP(launch_decode(a, want, c.stream));
+    LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost,
+                           c.stream));
+    LGS_HIP(hipStreamSynchronize(c.stream));
+    const uint8_t st = h[o_st];
+    if (st == LGS_ST_OK) memcpy(zp, h + o_out, want);
+    *ok = st == LGS_ST_OK;
+    return LGS_OK;
+  }
+  // Larger than the slot (multi-MiB index blocks): device memory for this
+  // call only, the stream uploaded straight from the caller's (pageable)
+  // buffer, and the output downloaded into zp only once the status says ok.
+  uint8_t* big = nullptr;
+  const size_t big_bytes = align_up((size_t)n + 16, 256) + align_up((size_t)want + 16, 256);
+  if (hipMalloc(&big, big_bytes) != hipSuccess)
+    return fail(LGS_ENOMEM, "hipMalloc(%zu) for a %u-byte block failed", big_bytes, want);
+  struct Free {
+    uint8_t* p;
+    ~Free() { (void)hipFree(p); }
+  } guard{big};
+  uint8_t* const d_in = big;
+  uint8_t* const d_out = big + align_up((size_t)n + 16, 256);
+  Layout M;                                                      // per-item arrays, in the slot
+  const size_t m_ioff = M.take(8), m_ilen = M.take(4), m_ooff = M.take(8), m_ocap = M.take(4);
+  const size_t m_up = M.at;
+  const size_t m_st = M.take(4), m_olen = M.take(4);
+  const size_t m_down = M.at;
+  uint8_t* const d = c.d_buf;
+  *(uint64_t*)(h + m_ioff) = 0;
+  *(uint32_t*)(h + m_ilen) = n;
+  *(uint64_t*)(h + m_ooff) = 0;
+  *(uint32_t*)(h + m_ocap) = want;
+  LGS_HIP(hipMemcpyAsync(d_in, xp, n, hipMemcpyHostToDevice, c.stream));
+  LGS_HIP(hipMemsetAsync(d_in + n, 0, 16, c.stream));
+  LGS_HIP(hipMemcpyAsync(d, h, m_up, hipMemcpyHostToDevice, c.stream));
+  DecodeArgs a{d_in, (const uint64_t*)(d + m_ioff), (const uint32_t*)(d + m_ilen), d_out,
+               (const uint64_t*)(d + m_ooff), (const uint32_t*)(d + m_ocap),
+               (uint32_t*)(d + m_olen), d + m_st, nullptr, 1, nullptr};
   LGS_HIP(launch_decode(a, want, c.stream));
-  LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + m_st, d + m_st, m_down - m_st, hipMemcpyDeviceToHost, c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
-  const uint8_t st = h[o_st];
-  if (st == LGS_ST_OK) memcpy(zp, h + o_out, want);
-  *ok = st == LGS_ST_OK;
+  if (h[m_st] == LGS_ST_OK) {
+    LGS_HIP(hipMemcpyAsync(zp, d_out, want, hipMemcpyDeviceToHost, c.stream));
+    LGS_HIP(hipStreamSynchronize(c.stream));
+    *ok = 1;
+  }
   return LGS_OK;
+}
+
+// Kernel options: lgs_set_option(), initial values from the environment.
+Options& options_init() {
+  static Options* o = [] {
+    Options* v = new Options;
+    const char* dk = getenv("LGS_DECODE_KERNEL");
+    if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
+    if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
+    const char* ns = getenv("LGS_NO_SPLIT");
+    if (ns && *ns && strcmp(ns, "0")) v->split = 0;
+    return v;
+  }();
+  return *o;
 }
 
 }  // namespace
 
 int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+Options& options() { return options_init(); }
 
 }  // namespace lgs
 
@@ -447,6 +702,8 @@ int ldb_snappy_encode_size(size_t* zn, size_t xn) {   // snappy.c:347-362
 }
 
 size_t ldb_snappy_encode(uint8_t* zp, const uint8_t* xp, size_t xn) {
+  // lcdb's encode path has no error return (table_builder.c:182-188): a
+  // failure here is a lost device or a broken runtime, so abort loudly.
   size_t written = 0;
   if (encode_one(zp, xp, xn, &written) != LGS_OK) die("ldb_snappy_encode");
   return written;
@@ -461,9 +718,48 @@ int ldb_snappy_decode_size(size_t* zn, const uint8_t* xp, size_t xn) {   // snap
 }
 
 int ldb_snappy_decode(uint8_t* zp, const uint8_t* xp, size_t xn) {
+  // format.c:237-251 turns 0 into LDB_CORRUPTION.  Running out of device
+  // memory for a block larger than a drop-in slot reports 0 as well (with a
+  // diagnostic): the reference cannot fail that way and lcdb has no other
+  // code for it.  Anything else is a lost device: abort loudly.
   int ok = 0;
-  if (decode_one(zp, xp, xn, &ok) != LGS_OK) die("ldb_snappy_decode");
+  const int rc = decode_one(zp, xp, xn, &ok);
+  if (rc == LGS_ENOMEM) {
+    fprintf(stderr, "lcdb_gpu_snappy: ldb_snappy_decode: %s\n", t_err);
+    return 0;
+  }
+  if (rc != LGS_OK) die("ldb_snappy_decode");
   return ok;
+}
+
+// ---- drop-in footprint and kernel options ----
+
+int lgs_dropin_footprint(size_t* pinned, size_t* device, uint32_t* slots, size_t* slot_bytes) {
+  if (!pinned || !device || !slots || !slot_bytes) return fail(LGS_EINVAL, "NULL argument");
+  unsigned n = 0;
+  dropin_pool().footprint(pinned, device, &n);
+  *slots = n;
+  *slot_bytes = dropin_pool().fixed_cap();
+  return LGS_OK;
+}
+
+int lgs_set_option(const char* name, const char* value) {
+  if (!name || !value) return fail(LGS_EINVAL, "NULL argument");
+  Options& o = options();
+  if (!strcmp(name, "decoder")) {
+    if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
+    else if (!strcmp(value, "ring")) o.decoder = kDecRing;
+    else if (!strcmp(value, "wave")) o.decoder = kDecWave;
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
+    return LGS_OK;
+  }
+  if (!strcmp(name, "split")) {
+    if (!strcmp(value, "1")) o.split = 1;
+    else if (!strcmp(value, "0")) o.split = 0;
+    else return fail(LGS_EINVAL, "split '%s' (0 or 1)", value);
+    return LGS_OK;
+  }
+  return fail(LGS_EINVAL, "unknown option '%s'", name);
 }
 
 // ---- batched API ----
@@ -501,8 +797,9 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   if (n == 0) return LGS_OK;
   if (!in || !in_off || !in_len || !out || !out_off || !out_len)
     return fail(LGS_EINVAL, "NULL argument");
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   size_t in_total = 0, out_total = 0;
   uint32_t max_in = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -560,8 +857,9 @@ int lgs_decode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   if (n == 0) return LGS_OK;
   if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !status)
     return fail(LGS_EINVAL, "NULL argument");
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   size_t in_total = 0, out_total = 0;
   uint32_t max_cap = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -762,8 +1060,9 @@ int lgs_table_write_host(const uint8_t* raw, const uint64_t* raw_off, const uint
     return fail(LGS_EINVAL, "NULL argument");
   if (compression != LGS_NO_COMPRESSION && compression != LGS_SNAPPY_COMPRESSION)
     return fail(LGS_EINVAL, "unknown compression type %d", compression);
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   size_t in_total = 0;
   uint32_t max_in = 0;
   for (uint32_t i = 0; i < n; ++i) {
@@ -875,8 +1174,9 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
   if (n == 0) return LGS_OK;
   if (!file || !handle_off || !handle_size || !out || !out_off || !out_cap || !out_len || !status)
     return fail(LGS_EINVAL, "NULL argument");
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   // Only each block's byte range (+ trailer) travels, packed 16-aligned;
   // a range outside the file keeps an out-of-range offset so the device
   // reports the truncated read itself (format.c:195-198).
@@ -1044,8 +1344,9 @@ int lgs_bloom_build_host(const uint8_t* keys, const uint64_t* key_off, const uin
     return fail(LGS_EINVAL, "bits_per_key %d out of range", bits_per_key);
   for (uint32_t f = 0; f < nfilters; ++f)
     if (first[f + 1] < first[f]) return fail(LGS_EINVAL, "first[] decreases at filter %u", f);
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   const uint32_t nkeys = first[nfilters] - first[0];
   const uint32_t k0 = first[0];
   size_t key_bytes = 0, filt_bytes = 0;
@@ -1107,8 +1408,9 @@ int lgs_bloom_match_host(const uint8_t* filters, const uint64_t* filter_off,
   for (uint32_t q = 0; q < nq; ++q)
     if (query_filter[q] >= nfilters)
       return fail(LGS_EINVAL, "query %u names filter %u of %u", q, query_filter[q], nfilters);
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   size_t fb = 0, kb = 0;
   for (uint32_t f = 0; f < nfilters; ++f) fb += filter_len[f];
   for (uint32_t q = 0; q < nq; ++q) kb += key_len[q];
@@ -1247,8 +1549,9 @@ int lgs_filter_block_build_host(const uint8_t* keys, const uint64_t* key_off,
   }
   const uint32_t k0 = block_first[0], nkeys = block_first[nblocks] - k0;
   if (nkeys && (!keys || !key_off || !key_len)) return fail(LGS_EINVAL, "NULL argument");
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   size_t key_bytes = 0;
   for (uint32_t i = k0; i < k0 + nkeys; ++i) key_bytes += key_len[i];
   const size_t bound = lgs_filter_block_bound(nkeys, nblocks, data_end, bits_per_key);
@@ -1323,8 +1626,9 @@ int lgs_filter_block_match_host(const uint8_t* block, size_t block_len,
   if (nq == 0) return LGS_OK;
   if ((block_len && !block) || !block_offset || !keys || !key_off || !key_len || !match)
     return fail(LGS_EINVAL, "NULL argument");
-  Ctx& c = t_ctx;
-  LGS_TRY(ctx_ready(c));
+  Lease lease(batch_pool());
+  LGS_TRY(lease.acquire());
+  Ctx& c = lease.ctx();
   size_t kb = 0;
   for (uint32_t q = 0; q < nq; ++q) kb += key_len[q];
   Layout L;
@@ -1361,17 +1665,13 @@ int lgs_filter_block_match_host(const uint8_t* block, size_t block_len,
   return LGS_OK;
 }
 
-int lgs_device_count(void) {
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess) return 0;
-  return count;
-}
+int lgs_device_count(void) { return visible_devices(); }
 
 int lgs_set_device(int device) {
   int count = lgs_device_count();
   if (device < 0 || device >= count)
     return fail(LGS_ENODEV, "device %d not present (%d visible)", device, count);
-  t_ctx.want_device = device;
+  t_want_device = device;
   return LGS_OK;
 }
 

@@ -18,8 +18,7 @@
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
-#include <stdlib.h>
-#include <string.h>
+#include <mutex>
 
 namespace lgs {
 
@@ -286,31 +285,11 @@ __device__ __forceinline__ void flush_out(gptr<uint8_t> dst, const uint8_t* o, u
 }
 
 // ---------------------------------------------------------------------------
-// Lane-per-block decoder (large batches of small blocks).
-//
-// One LANE decodes one whole block, straight from HBM to HBM: the tag walk
-// is per-lane VALU code, so one instruction advances up to 64 blocks (the
-// wave-per-block kernel above is bound by the CU's single scalar unit:
-// ~60 SALU instructions per tag).
-//
-// With 65 536 blocks a CU holds only ~4 such waves, so each block's serial
-// chain of ~180 tags is the critical path and what it costs per tag is
-// memory round trips.  Each tag therefore issues every load it needs at once
-// -- the 16-byte view of the NEXT tag and up to four 16-byte chunks of the
-// source (literal bytes from the input, or copy bytes from this block's
-// earlier output) -- and waits once.  vmcnt also counts stores and retires
-// in issue order, so a load issued after a store waits for it: a loop of
-// load/store pairs would pay one round trip per 16 bytes.
-//
-// Writes may run up to 15 bytes past the current op ("wild" chunks) because
-// later ops overwrite them; they never pass the block's end (the last chunk
-// is written byte-exact).  A copy reads bytes this lane stored earlier
-// (same-work-item program order).  Overlapping copies (dist < len) keep a
-// sequential path: dist == 1 broadcasts a byte (all of fillseq's), dist < 16
-// builds the period in registers, dist >= 16 copies chunk after chunk.
-//
-// Reads may touch 16 bytes past a block's input and past its output cursor
-// (see lgs_decode_batch_dev).
+// Per-lane helpers of the ring decoder below (one lane decodes one block).
+// Reads may touch 16 bytes past a block's input (see lgs_decode_batch_dev).
+// (A kernel that moved every byte as a 16-byte global access of its own
+// lane, straight HBM to HBM, ran C2 at 373 GiB/s: its texture addresser was
+// 93 % busy and 3.4x the output bytes reached HBM.  Removed in round 2.)
 // ---------------------------------------------------------------------------
 typedef u32x4 u32x4_u __attribute__((aligned(1)));
 
@@ -349,18 +328,6 @@ __device__ __forceinline__ void st_exact(gptr<uint8_t> p, u32x4 v, uint32_t len)
     const uint32_t byte = byte_of(v, b);
     asm volatile("global_store_byte %0, %1, off\n\ts_nop 1" ::"v"(p + b), "v"(byte)
                  : "memory");
-  }
-}
-
-// Chunk k (16 bytes at d + 16k) of an op whose output ends `room` bytes
-// after d's block end would allow: wild when it fits, byte-exact otherwise.
-__device__ __forceinline__ void put16(gptr<uint8_t> d, u32x4 v, uint32_t k, uint32_t len,
-                                      uint32_t room) {
-  if (16 * k + 16 <= room) {
-    st16(d + 16 * k, v);
-  } else {
-    const uint32_t r = len - 16 * k;
-    st_exact(d + 16 * k, v, r < 16 ? r : 16);
   }
 }
 
@@ -404,185 +371,6 @@ __device__ __forceinline__ Tag parse_tag(u32x4 tv, uint32_t pos, uint32_t slen, 
   t.bad = lit ? lbad : cbad;
   t.next = pos + t.hl + (lit ? t.len : 0u);
   return t;
-}
-
-// Overlapping copies whose period does not divide 16 (dist 3, 5-7, 9-15)
-// or is >= 16: the only ops the fast path does not take.
-__device__ __forceinline__ bool tag_slow(const Tag& t) {
-  return t.kind != 0 && t.dist < t.len && !(t.dist <= 8 && (t.dist & (t.dist - 1)) == 0);
-}
-
-// Fast path for one tag: every load it needs (up to four 16-byte source
-// chunks and the next tag's view) in one round trip, one explicit wait,
-// then the stores.  Literals over 64 bytes continue 64 bytes a trip.
-// Returns the next tag's view.
-__device__ __forceinline__ u32x4 fast_op(const Tag& t, gptr<const uint8_t> src, uint32_t pos,
-                                         gptr<uint8_t> d, uint32_t room) {
-  const uint32_t len = t.len, dist = t.dist;
-  const bool overlap = t.kind != 0 && dist < len;               // dist 1, 2, 4 or 8 here
-  const gptr<const uint8_t> sp = t.kind == 0 ? src + pos + t.hl : (gptr<const uint8_t>)(d - dist);
-  // (Zero-initialised, not copies of c0: a copy would make the compiler wait
-  // for c0 before issuing the rest.)
-  const u32x4 c0 = ld16(sp);
-  u32x4 c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;
-  if (!overlap) {
-    if (len > 16) c1 = ld16(sp + 16);
-    if (len > 32) c2 = ld16(sp + 32);
-    if (len > 48) c3 = ld16(sp + 48);
-  }
-  const u32x4 tn = ld16(src + t.next);
-  // The tag's one wait.  Explicit, so that the compiler knows every chunk
-  // and the next view have arrived: its own waits in front of the
-  // (exec-masked, so not exactly countable) stores below would be vmcnt(1)s
-  // that wait for the previous store at each step.
-  __builtin_amdgcn_s_waitcnt(0x0f70);                           // vmcnt(0)
-
-  // Overlapping copies of period 1/2/4/8 (every one in fillseq is dist 1):
-  // the pattern of the dist bytes before d, as a 16-byte register.
-  const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
-  const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
-  const uint32_t px = dist == 1 ? w1 : (dist == 2 ? w2 : c0.x);
-  const uint32_t py = dist == 8 ? c0.y : px;
-  const u32x4 pv = {px, py, px, py};
-  const u32x4 v0 = overlap ? pv : c0, v1 = overlap ? pv : c1, v2 = overlap ? pv : c2,
-              v3 = overlap ? pv : c3;
-  put16(d, v0, 0, len, room);
-  if (len > 16) put16(d, v1, 1, len, room);
-  if (len > 32) put16(d, v2, 2, len, room);
-  if (len > 48) put16(d, v3, 3, len, room);
-  if (len > 64) {
-    // Literals longer than 64 bytes (copies never are).
-#pragma clang loop unroll(disable)
-    for (uint32_t k = 4; 16 * k < len; k += 4) {
-      const u32x4 e0 = ld16(sp + 16 * k);
-      u32x4 e1 = {0, 0, 0, 0}, e2 = e1, e3 = e1;
-      if (len > 16 * k + 16) e1 = ld16(sp + 16 * k + 16);
-      if (len > 16 * k + 32) e2 = ld16(sp + 16 * k + 32);
-      if (len > 16 * k + 48) e3 = ld16(sp + 16 * k + 48);
-      __builtin_amdgcn_s_waitcnt(0x0f70);
-      put16(d, e0, k, len, room);
-      if (len > 16 * k + 16) put16(d, e1, k + 1, len, room);
-      if (len > 16 * k + 32) put16(d, e2, k + 2, len, room);
-      if (len > 16 * k + 48) put16(d, e3, k + 3, len, room);
-    }
-  }
-  return tn;
-}
-
-// Slow path: overlapping copies of other periods, in the reference's byte
-// order (snappy.c:329-330).  Returns the next tag's view.
-__device__ __noinline__ u32x4 slow_op(const Tag& t, gptr<const uint8_t> src, gptr<uint8_t> d,
-                                      uint32_t room) {
-  const uint32_t len = t.len, dist = t.dist;
-  const gptr<const uint8_t> sp = (gptr<const uint8_t>)(d - dist);
-  if (dist >= 16) {
-    // Each chunk's source was written by an earlier chunk of this op.
-#pragma clang loop unroll(disable)
-    for (uint32_t k = 0; 16 * k < len; ++k) put16(d, ld16(sp + 16 * k), k, len, room);
-  } else {
-    // p = the first 16 bytes of the pattern; bytes x and x - q agree for
-    // q = dist * ceil(16 / dist) >= 16, so later chunks copy from q back.
-    const u32x4 c0 = ld16(sp);
-    uint32_t w[4] = {0, 0, 0, 0};
-    uint32_t r = 0;
-#pragma clang loop unroll(disable)
-    for (uint32_t j = 0; j < 16; ++j) {
-      w[j >> 2] |= byte_of(c0, r) << (8 * (j & 3u));
-      r = r + 1 == dist ? 0 : r + 1;
-    }
-    put16(d, u32x4{w[0], w[1], w[2], w[3]}, 0, len, room);
-    const uint32_t q = dist * ((16 + dist - 1) / dist);
-#pragma clang loop unroll(disable)
-    for (uint32_t k = 1; 16 * k < len; ++k)
-      put16(d, ld16((gptr<const uint8_t>)(d + 16 * k - q)), k, len, room);
-  }
-  const u32x4 tn = ld16(src + t.next);
-  __builtin_amdgcn_s_waitcnt(0x0f70);
-  return tn;
-}
-
-template <uint32_t LANES>
-__global__ __launch_bounds__(64) void decode_lane_kernel(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
-    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
-    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
-    const uint32_t* __restrict__ index, uint32_t n) {
-  if (threadIdx.x >= LANES) return;
-  const uint32_t slot = blockIdx.x * LANES + threadIdx.x;
-  if (slot >= n) return;
-  const uint32_t i = index ? index[slot] : slot;
-  const gptr<const uint8_t> src = to_global(in) + in_off[i];
-  const uint32_t slen = in_len[i];
-  const gptr<uint8_t> dst = to_global(out) + out_off[i];
-  const uint32_t cap = out_cap[i];
-
-  // varint32 header, coding.h:169-204.
-  uint32_t st = 1, want = 0, hlen = 0;
-  {
-    const uint64_t h = view8(src);
-    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
-      const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
-      if ((b & 0x80u) == 0) {
-        want |= b << (7 * k);
-        hlen = k + 1;
-        break;
-      }
-      want |= (b & 0x7fu) << (7 * k);
-    }
-    if (hlen == 0 || want > 0x7fffffffu) st = 0;                // snappy.c:405-409
-    else if (want > cap) st = 2;
-    want = st == 1 ? want : 0;
-  }
-  // A lane that is not decoding (bad header, or done) has pos >= slen; a bad
-  // tag sets pos to a sentinel past slen (a sentinel rather than a status
-  // variable: one less loop-carried value).
-  uint32_t pos = st == 1 ? hlen : 0xffffffffu;
-  uint32_t made = 0;
-  u32x4 tv = ld16(src + (st == 1 ? pos : 0));
-  // Settle that load here: left pending into the loop, it makes the
-  // compiler wait vmcnt(0) at the loop head on every tag -- i.e. for the
-  // previous tag's stores too.
-  __builtin_amdgcn_s_waitcnt(0x0f70);
-
-  // Fast trips until some lane's next tag needs the slow path; then one
-  // trip in which every live lane does its op (slow or fast); repeat.  The
-  // fast loop holds no slow-path code, so the compiler's wait analysis sees
-  // nothing in flight at its head (a wait there would also wait for the
-  // previous tag's stores).
-  for (;;) {
-    Tag t;
-    bool live, slow_trip = false;
-    for (;;) {                                                  // snappy.c:208
-      live = pos < slen;
-      if (ballot(live) == 0) break;
-      t = parse_tag(tv, pos, slen, want, made);
-      if (live && t.bad) {
-        pos = 0xffffffffu;
-        live = false;
-      }
-      if (ballot(live && tag_slow(t))) {
-        slow_trip = true;
-        break;
-      }
-      if (live) {
-        tv = fast_op(t, src, pos, dst + made, want - made);
-        made += t.len;
-        pos = t.next;
-      }
-    }
-    if (!slow_trip) break;
-    if (live) {
-      tv = tag_slow(t) ? slow_op(t, src, dst + made, want - made)
-                       : fast_op(t, src, pos, dst + made, want - made);
-      made += t.len;
-      pos = t.next;
-    }
-  }
-  if (st == 1) st = (pos == slen && made == want) ? 1u : 0u;   // snappy.c:208, :337
-
-  status[i] = (uint8_t)st;
-  out_len[i] = st == 1 ? want : 0;
 }
 
 template <uint32_t OUT_CAP, uint32_t WAVES>
@@ -1093,23 +881,13 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
 }
 
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
-  // Default: two op slots per trip, 32 blocks per wave (rings for 32 lanes,
-  // 20 KB of LDS: eight waves fit a CU, two per SIMD, and each hides the
-  // other's memory waits).  LGS_DECODE_KERNEL=ring64: 64 blocks per wave
-  // (one per SIMD); ring1: that with one op slot (A/B).
-  const char* v = getenv("LGS_DECODE_KERNEL");
-  if (v && !strcmp(v, "ring1"))
-    hipLaunchKernelGGL((decode_ring_kernel<false, 64>), dim3((a.n + 63) / 64), dim3(64), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
-                       a.status, a.index, a.n, a.count);
-  else if (v && !strcmp(v, "ring64"))
-    hipLaunchKernelGGL((decode_ring_kernel<true, 64>), dim3((a.n + 63) / 64), dim3(64), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
-                       a.status, a.index, a.n, a.count);
-  else
-    hipLaunchKernelGGL((decode_ring_kernel<true, 32>), dim3((a.n + 31) / 32), dim3(64), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len,
-                       a.status, a.index, a.n, a.count);
+  // Two op slots per trip, 32 blocks per wave: the rings for 32 lanes take
+  // 20 KB of LDS, so eight waves fit a CU, two per SIMD, and each hides the
+  // other's memory waits.  (64 blocks per wave: 746 -> 709 GiB/s on C2; one
+  // op slot: 632.  Those variants were removed in round 2.)
+  hipLaunchKernelGGL((decode_ring_kernel<true, 32>), dim3((a.n + 31) / 32), dim3(64), 0, s, a.in,
+                     a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
+                     a.index, a.n, a.count);
   return hipGetLastError();
 }
 
@@ -1120,14 +898,6 @@ constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoo
 // Batches of at least this many blocks go to the lane-per-block kernel
 // (one wave per 64 blocks still fills the chip).
 constexpr uint32_t kLaneMinBlocks = 16384;
-
-template <uint32_t LANES>
-static hipError_t launch_decode_lane(const DecodeArgs& a, hipStream_t s) {
-  const uint32_t grid = (a.n + LANES - 1) / LANES;
-  hipLaunchKernelGGL((decode_lane_kernel<LANES>), dim3(grid), dim3(64), 0, s, a.in, a.in_off,
-                     a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------------------
 // Mixed-size batches.  One launch sized for its largest block runs every
@@ -1165,32 +935,50 @@ hipError_t launch_classify(const uint32_t* len, uint32_t n, uint32_t b0, uint32_
   return hipGetLastError();
 }
 
-hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
-  // Keep freed blocks in the device's default pool, so a split launch does
-  // not map memory every time.
-  static thread_local int tuned = -1;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (tuned != dev) {
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-    tuned = dev;
+// One private pool per device, created on first use and kept: freed
+// scratch stays mapped (release threshold 256 MiB), so a split launch does
+// not map memory every time.
+static hipMemPool_t scratch_pool(int dev, hipError_t* err) {
+  static std::mutex mu;
+  static hipMemPool_t pools[64] = {};
+  std::lock_guard<std::mutex> g(mu);
+  if (dev < 0 || dev >= 64) {
+    *err = hipErrorInvalidDevice;
+    return nullptr;
   }
-  return hipMallocAsync(p, bytes, s);
+  if (!pools[dev]) {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t p = nullptr;
+    if ((*err = hipMemPoolCreate(&p, &props)) != hipSuccess) return nullptr;
+    uint64_t keep = 256ull << 20;
+    (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+    pools[dev] = p;
+  }
+  *err = hipSuccess;
+  return pools[dev];
+}
+
+Scratch::Scratch(size_t bytes, hipStream_t s) : s_(s) {
+  int dev = 0;
+  err_ = hipGetDevice(&dev);
+  if (err_ != hipSuccess) return;
+  hipMemPool_t pool = scratch_pool(dev, &err_);
+  if (err_ != hipSuccess) return;
+  err_ = hipMallocFromPoolAsync(&p_, bytes, pool, s);
+  if (err_ != hipSuccess) p_ = nullptr;
 }
 
 #define LGS_TRY(x) do { const hipError_t e_ = (x); if (e_ != hipSuccess) return e_; } while (0)
 
 static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
-  void* scratch = nullptr;
   const size_t list_bytes = (size_t)4 * a.n * sizeof(uint32_t);
-  LGS_TRY(scratch_alloc(&scratch, list_bytes + 16, s));
-  uint32_t* list = (uint32_t*)scratch;
-  uint32_t* cnt = (uint32_t*)((uint8_t*)scratch + list_bytes);
+  Scratch scratch(list_bytes + 16, s);
+  LGS_TRY(scratch.status());
+  uint32_t* list = (uint32_t*)scratch.get();
+  uint32_t* cnt = (uint32_t*)((uint8_t*)scratch.get() + list_bytes);
   LGS_TRY(hipMemsetAsync(cnt, 0, 16, s));
   LGS_TRY(launch_classify(a.out_cap, a.n, kDecCap0, kDecCap1, kDecCap2, list, cnt, s));
   DecodeArgs c = a;
@@ -1208,22 +996,17 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
                        c.out, c.out_off, c.out_cap, c.out_len, c.status, c.index, c.n, c.count);
     LGS_TRY(hipGetLastError());
   }
-  return hipFreeAsync(scratch, s);
+  return scratch.release();
 }
 
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const char* force = getenv("LGS_DECODE_KERNEL");   // "ring" | "wave" | "lane64" | ...
-  if (!force && !a.index && max_out > kDecCap0 && a.n >= kSplitMinBlocks && !getenv("LGS_NO_SPLIT"))
+  const int force = options().decoder.load(std::memory_order_relaxed);
+  if (force == kDecAuto && !a.index && max_out > kDecCap0 && a.n >= kSplitMinBlocks &&
+      options().split.load(std::memory_order_relaxed))
     return launch_decode_split(a, max_out, s);
-  if (force) {
-    if (!strncmp(force, "ring", 4)) return launch_decode_ring(a, s);
-    if (!strcmp(force, "lane64")) return launch_decode_lane<64>(a, s);
-    if (!strcmp(force, "lane32")) return launch_decode_lane<32>(a, s);
-    if (!strcmp(force, "lane16")) return launch_decode_lane<16>(a, s);
-  } else if (a.n >= kLaneMinBlocks) {
+  if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))
     return launch_decode_ring(a, s);
-  }
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 1>(a, s);
   if (max_out <= kDecCap2) return launch_decode_cls<kDecCap2, 1>(a, s);

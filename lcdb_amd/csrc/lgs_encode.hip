@@ -26,9 +26,6 @@
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
-#include <stdlib.h>
-#include <string.h>
-
 namespace lgs {
 
 __constant__ ProbeTable kProbe = ProbeTable();
@@ -114,72 +111,6 @@ __device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uin
   }
   return total;
 }
-
-// snappy.c:53-102, the common case: the pending literal x[lit .. lit+L)
-// (L == 0: none) followed by a copy of length C < 68 at distance D (C == 0:
-// none), written 64 bytes a pass: lane b writes byte b of the sequence.
-// The header and tag arithmetic runs on the VALU (vec()), and every ?:
-// picks between values already computed (clang lowers a conditional whose
-// arms still hold work to exec-mask branches, whose save/restore is scalar
-// work -- and the scalar unit is what this kernel saturates).  Lanes past
-// the end store at an out-of-range offset that the buffer range check
-// drops.  pass(0) is straight-line code the caller can place next to other
-// LDS work; total > 64 needs further passes (rare).
-struct Seq {
-  uint32_t vL, vD, vlit, hl, hdr, has60, first, lend, vtotal, total;
-  __device__ __forceinline__ Seq(uint32_t lit, uint32_t L, uint32_t D, uint32_t C) {
-    vL = vec(L);
-    vD = vec(D);
-    vlit = vec(lit);
-    const uint32_t vC = vec(C);
-    const uint32_t m = vL - 1;                                        // snappy.c:55-66
-    const uint32_t hl_big = m < 256 ? 2u : 3u;
-    const uint32_t hl_any = m < 60 ? 1u : hl_big;
-    hl = vL == 0 ? 0u : hl_any;
-    const uint32_t h0_big = m < 256 ? 0xf0u : 0xf4u;
-    const uint32_t m4 = m << 2;
-    const uint32_t h0 = m < 60 ? m4 : h0_big;
-    hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);
-    has60 = vC > 64 ? 3u : 0u;                                        // snappy.c:84-89
-    const uint32_t rest = vC - 20 * has60;
-    // rest < 12 && D < 2048 (snappy.c:91), as sign bits: no lane-mask logic.
-    const bool c1 = (int32_t)((rest - 12) & (vD - 2048)) < 0;
-    const uint32_t f1 = ((vD >> 8) << 5) | ((rest - 4) << 2) | 1u;    // snappy.c:98
-    const uint32_t f2 = ((rest - 1) << 2) | 2u;                       // snappy.c:92
-    first = c1 ? f1 : f2;
-    const uint32_t ntag = c1 ? 2u : 3u;
-    const uint32_t ctag = has60 + ntag;
-    const uint32_t ctot = vC == 0 ? 0u : ctag;
-    lend = hl + vL;                                                   // first copy byte
-    vtotal = lend + ctot;
-    total = uni(vtotal);
-  }
-  __device__ __forceinline__ void pass(const OutSlot& o, uint32_t op, const uint8_t* x,
-                                       uint32_t n, uint32_t j0) const {
-    const uint32_t b = vec(j0) + lane_id();
-    const uint32_t ia = vlit + b - hl;                                // underflows for b < hl
-    const uint32_t iac = ia < n ? ia : n;
-    const uint32_t lb = x[iac];
-    const uint32_t cb = b - lend;                                     // byte of the copy tags
-    const uint32_t r = cb - has60;
-    const uint32_t dlo = vD, dhi = vD >> 8;
-    const uint32_t t60 = cb == 1 ? dlo : dhi;
-    const uint32_t p60 = cb == 0 ? 0xeeu : t60;                       // the 60-byte piece
-    const uint32_t tr = r == 1 ? dlo : dhi;
-    const uint32_t pr = r == 0 ? first : tr;                          // the final piece
-    const uint32_t cv = cb < has60 ? p60 : pr;
-    const uint32_t hb = hdr >> ((8 * b) & 31);
-    const uint32_t bv = b < lend ? lb : cv;
-    const uint32_t v = b < hl ? hb : bv;
-    const uint32_t voff = b < vtotal ? b : 0x40000000u;               // dropped by the range check
-    o.put(op, voff, v);
-  }
-  __device__ __forceinline__ void rest(const OutSlot& o, uint32_t op, const uint8_t* x,
-                                       uint32_t n) const {
-#pragma clang loop unroll(disable) vectorize(disable)
-    for (uint32_t j0 = kWave; j0 < total; j0 += kWave) pass(o, op, x, n, j0);
-  }
-};
 
 // The recorded ops of one chunk, emitted lane-parallel: lane k holds op k
 // (recA = copy start << 16 | copy length, recB = copy distance), each op
@@ -321,14 +252,11 @@ constexpr uint32_t kSink = kTableCap;
 // share no hash with an earlier lane; the first lane never does).  Among the
 // committed probes each group's latest member writes the table.
 //
-// A found match is extended, then its literal and copy are emitted in one
-// pass (emit_seq), then lcdb's immediate re-probe runs (snappy.c:172-186)
-// as identical work on every lane.
-//
-// DEFER: instead of emitting each literal + copy inside the next batch,
-// record the op in lane registers (v_writelane) and emit 64 ops at a time
-// lane-parallel (flush_ops): a few VALU per op instead of one 64-lane pass.
-template <bool DEFER>
+// A found match is extended; lcdb's immediate re-probe (snappy.c:172-186)
+// is folded into the next batch (below).  The literal + copy is not emitted
+// on the spot: the op is recorded in lane registers (v_writelane) and 64 ops
+// at a time are emitted lane-parallel (flush_ops), a few VALU per op instead
+// of one 64-lane pass.  (The per-op pass measured 176 against 213 GiB/s.)
 __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
                                  const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
   const uint32_t lane = lane_id();
@@ -348,9 +276,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
   uint32_t at = 0;       // end of the last copy
   uint32_t start = 1;    // first probe position of the current search (snappy.c:112)
   uint32_t kv = 2;       // virtual probe index of this batch's first lane
-  // The last copy's emission, deferred into the next batch (below).
-  uint32_t e_lit = 0, e_L = 0, e_D = 0, e_C = 0, e_longlen = 0;
-  // DEFER: recorded ops (lane k = op k), their count, op 0's literal start.
+  // Recorded ops (lane k = op k), their count, op 0's literal start.
   uint32_t recA = 0, recB = 0, nops = 0, lit0 = 0;
 
   // Each batch takes 64 consecutive probes of a virtual sequence:
@@ -384,13 +310,6 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
       // until the previous copy's bytes had reached memory.
       __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
     }
-    // The previous copy's literal + tags (snappy.c:156, :166), emitted here
-    // as straight-line code in the batch's first block, so that it fills the
-    // batch's LDS waits instead of lengthening the copy -> batch chain.
-    // (Nothing pending: a zero-length sequence, every store dropped.)
-    const Seq sq(e_lit, e_L, e_D, e_C);
-    if (!DEFER) sq.pass(o, op, x, n, 0);
-
     const bool isA = v == 0, isB = v == 1;
     const bool valid = v < 2 || (in_tab && start + o1 <= last);  // snappy.c:143
     const uint64_t vmask = ballot(valid);
@@ -448,12 +367,6 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     order();
     tab[((pi < ncommit) & !shadowed) ? hh : kSink] = (uint16_t)p;
     order();
-    if (!DEFER) {
-      sq.rest(o, op, x, n);                                       // rare: > 64 bytes
-      op += sq.total;
-      if (e_longlen) op += emit_copy(o, op, e_D, e_longlen);      // rare: 68+ byte copy
-      e_L = e_C = e_longlen = 0;
-    }
 
     // The match path computes the copy's end; both paths then update the
     // loop state with selects (one set of loop-carried values, no per-path
@@ -483,23 +396,13 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
       }
 
       // snappy.c:156 + 166: the literal before the copy (empty after a
-      // re-match), then the copy -- emitted during the next batch (copies
-      // of 68+ bytes, rare, get their tags from emit_copy).
+      // re-match), then the copy -- recorded, emitted by flush_ops.
       const uint32_t clen = at_n - base, dist = base - ref;
-      if (DEFER) {
-        write_lane2(recA, (base << 16) | clen, recB, dist, nops);
-        if (++nops == kWave) {                                    // every 64 ops
-          op = flush_ops(o, op, x, recA, recB, kWave, lit0);
-          nops = 0;
-          lit0 = at_n;
-        }
-      } else {
-        const bool longc = clen >= 68;
-        e_lit = lit;
-        e_L = base - lit;
-        e_D = dist;
-        e_C = longc ? 0u : clen;
-        e_longlen = longc ? clen : 0u;
+      write_lane2(recA, (base << 16) | clen, recB, dist, nops);
+      if (++nops == kWave) {                                      // every 64 ops
+        op = flush_ops(o, op, x, recA, recB, kWave, lit0);
+        nops = 0;
+        lit0 = at_n;
       }
     }
     // Match: the search restarts after the copy (snappy.c:169, 184-185).
@@ -512,15 +415,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     at = at_n;
     if (done) break;
   }
-  if (DEFER) {
-    if (nops) op = flush_ops(o, op, x, recA, recB, nops, lit0);
-  } else {                                                        // the last copy's emission
-    const Seq sq(e_lit, e_L, e_D, e_C);
-    sq.pass(o, op, x, n, 0);
-    sq.rest(o, op, x, n);
-    op += sq.total;
-    if (e_longlen) op += emit_copy(o, op, e_D, e_longlen);
-  }
+  if (nops) op = flush_ops(o, op, x, recA, recB, nops, lit0);
 
   if (lit < n) op += emit_literal(o, op, x, lit, n - lit);         // snappy.c:190-192
   return op;
@@ -529,7 +424,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
 // Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
 // its varint32 length (snappy.c:368).  Otherwise hdr[i] is the varint value
 // to prefix, or 0xffffffff for none (a later chunk of a > 64 KiB block).
-template <uint32_t IN_CAP, uint32_t WAVES, bool DEFER>
+template <uint32_t IN_CAP, uint32_t WAVES>
 __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -582,7 +477,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* x = &s_in[wv][sh];
     order();
     if (clen >= kMinBlock) {
-      op = encode_chunk<DEFER>(x, clen, &s_tab[wv][0], o, op, off0, off1);
+      op = encode_chunk(x, clen, &s_tab[wv][0], o, op, off0, off1);
     } else {
       op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
@@ -591,34 +486,12 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   if (lane == 0) out_len[i] = op;
 }
 
-// Gather kernel for > 64 KiB blocks: piece p (one chunk's encoded bytes,
-// src + src_off[p], src_len[p]) is appended at dst + dst_off[p].
-__global__ __launch_bounds__(256) void concat_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, uint32_t n) {
-  const uint32_t p = blockIdx.x;
-  if (p >= n) return;
-  const gptr<const uint8_t> s = to_global(src) + src_off[p];
-  const gptr<uint8_t> d = to_global(dst) + dst_off[p];
-  const uint32_t len = src_len[p];
-  for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) d[j] = s[j];
-}
-
 template <uint32_t IN_CAP, uint32_t WAVES>
 static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
   const uint32_t grid = (a.n + WAVES - 1) / WAVES;
-  // LGS_ENCODE_EMIT=inline: the per-batch emission variant (A/B).
-  const char* emit = getenv("LGS_ENCODE_EMIT");
-  if (emit && !strcmp(emit, "inline")) {
-    hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES, false>), dim3(grid), dim3(64 * WAVES), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
-                       a.count);
-  } else {
-    hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES, true>), dim3(grid), dim3(64 * WAVES), 0, s,
-                       a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
-                       a.count);
-  }
+  hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s, a.in,
+                     a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
+                     a.count);
   return hipGetLastError();
 }
 
@@ -628,27 +501,21 @@ constexpr uint32_t kEncCap2 = 65536;
 
 // max_in: largest item length in the launch (<= 65536).
 // Blocks longer than 64 KiB are encoded chunk by chunk by their wave.
-// LGS_ENCODE_KERNEL=wave|group16|group32|group64 forces a variant (A/B).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  const char* force = getenv("LGS_ENCODE_KERNEL");
-  if (force && !strncmp(force, "group", 5)) {
-    const hipError_t e = launch_encode_group(a, max_in, (uint32_t)atoi(force + 5), s);
-    if (e != hipErrorNotSupported) return e;
-  }
   if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
-  if (a.index || a.n < kSplitMinBlocks || getenv("LGS_NO_SPLIT")) {
+  if (a.index || a.n < kSplitMinBlocks || !options().split) {
     if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
     return launch_encode_cls<kEncCap2, 1>(a, s);
   }
   // A mixed-size batch: each size class in its own kernel (see
   // launch_decode_split), so small blocks keep their small LDS images.
-  void* scratch = nullptr;
   const size_t list_bytes = (size_t)3 * a.n * sizeof(uint32_t);
-  hipError_t e = scratch_alloc(&scratch, list_bytes + 16, s);
+  Scratch scratch(list_bytes + 16, s);
+  hipError_t e = scratch.status();
   if (e != hipSuccess) return e;
-  uint32_t* list = (uint32_t*)scratch;
-  uint32_t* cnt = (uint32_t*)((uint8_t*)scratch + list_bytes);
+  uint32_t* list = (uint32_t*)scratch.get();
+  uint32_t* cnt = (uint32_t*)((uint8_t*)scratch.get() + list_bytes);
   EncodeArgs c = a;
   if ((e = hipMemsetAsync(cnt, 0, 16, s)) != hipSuccess ||
       (e = launch_classify(a.in_len, a.n, kEncCap0, kEncCap1, 0xffffffffu, list, cnt, s)) !=
@@ -660,15 +527,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if ((e = launch_encode_cls<kEncCap1, 1>(c, s)) != hipSuccess) return e;
   c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
   if (max_in > kEncCap1 && (e = launch_encode_cls<kEncCap2, 1>(c, s)) != hipSuccess) return e;
-  return hipFreeAsync(scratch, s);
-}
-
-hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
-                         uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(concat_kernel, dim3(n), dim3(256), 0, s, src, src_off, src_len, dst,
-                     dst_off, n);
-  return hipGetLastError();
+  return scratch.release();
 }
 
 }  // namespace lgs

@@ -7,7 +7,19 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
+
 namespace lgs {
+
+// Process-wide kernel choices (lgs_set_option; the initial values come from
+// LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
+// launch path reads the environment).
+enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2 };
+struct Options {
+  std::atomic<int> decoder{kDecAuto};   // DecodeKernel
+  std::atomic<int> split{1};            // size-class split of mixed batches
+};
+Options& options();
 
 struct DecodeArgs {
   const uint8_t* in; const uint64_t* in_off; const uint32_t* in_len;
@@ -27,10 +39,6 @@ struct EncodeArgs {
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
 // max_in: largest item length in the launch (<= 65536).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s);
-// Several-blocks-per-wave encoder (lgs_encode_group.hip); lanes per block =
-// 16, 32 or 64.  hipErrorNotSupported if the batch does not qualify.
-hipError_t launch_encode_group(const EncodeArgs& a, uint32_t max_in, uint32_t lanes,
-                               hipStream_t s);
 // Sort a mixed-size batch into size classes on the device: class c holds
 // the items with len in (b[c-1], b[c]] (b[3] = infinity); list[c * n + k]
 // is its k-th item (in no particular order), cnt[c] its size.  cnt must be
@@ -41,10 +49,29 @@ hipError_t launch_encode_group(const EncodeArgs& a, uint32_t max_in, uint32_t la
 constexpr uint32_t kSplitMinBlocks = 512;
 hipError_t launch_classify(const uint32_t* len, uint32_t n, uint32_t b0, uint32_t b1, uint32_t b2,
                            uint32_t* list, uint32_t* cnt, hipStream_t s);
-// Stream-ordered scratch for a split launch (one device's pool, kept warm).
-hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
-hipError_t launch_concat(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
-                         uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s);
+// Stream-ordered scratch of a split launch, from a private memory pool of
+// the current device (the process's default pool is left alone: this
+// library is loaded into lcdb).  Freed on the stream when the guard leaves
+// scope, on every path; release() frees it early and reports the error.
+class Scratch {
+ public:
+  Scratch(size_t bytes, hipStream_t s);
+  ~Scratch() { (void)release(); }
+  Scratch(const Scratch&) = delete;
+  Scratch& operator=(const Scratch&) = delete;
+  hipError_t status() const { return err_; }
+  void* get() const { return p_; }
+  hipError_t release() {
+    void* p = p_;
+    p_ = nullptr;
+    return p ? hipFreeAsync(p, s_) : hipSuccess;
+  }
+
+ private:
+  void* p_ = nullptr;
+  hipStream_t s_;
+  hipError_t err_;
+};
 
 // ---- SSTable block framing (lgs_table.hip) ----
 

@@ -56,3 +56,18 @@ def gpu():
         pytest.fail("gpu test needs a visible MI355X (lgs_device_count() == 0)")
     from lcdb_amd import snappy
     return snappy
+
+
+@pytest.fixture
+def force():
+    """force(name, value): lgs_set_option for one test, reset afterwards."""
+    from lcdb_amd import _native
+    touched = []
+
+    def set_(name: str, value: str) -> None:
+        _native.set_option(name, value)
+        touched.append(name)
+
+    yield set_
+    for name in touched:
+        _native.set_option(name, {"decoder": "auto", "split": "1"}[name])

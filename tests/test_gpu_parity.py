@@ -33,7 +33,7 @@ def test_dropin_decode_golden(gpu, vectors):
 
 
 def test_dropin_ramp_known_answer(gpu, digests):
-    # t-snappy.c:24-53 (1 MiB input: 16 chunks of 64 KiB, concatenated on device)
+    # t-snappy.c:24-53 (1 MiB input: 16 chunks of 64 KiB, one drop-in pass)
     data = bytes(i & 0xFF for i in range(1 << 20))
     enc = gpu.encode(data)
     assert len(enc) == 53203
@@ -197,11 +197,11 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lane64", "lane32", "ring", "ring1", "ring64"])
-def test_decode_kernel_variants_golden(gpu, vectors, kernel, monkeypatch):
-    # Every decode kernel (forced through LGS_DECODE_KERNEL) against the
+@pytest.mark.parametrize("kernel", ["wave", "ring"])
+def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
+    # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
-    monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+    force("decoder", kernel)
     enc = [v for v in vectors if v.kind == 0]
     res, st = gpu.decode_batch_host([v.b for v in enc], [len(v.a) for v in enc])
     for v, o, s in zip(enc, res, st):
@@ -216,7 +216,7 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, monkeypatch):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
+def test_decode_kernels_c2_full_size(gpu, digests, force):
     import torch
     from lcdb_amd import batch
     d = digests["C2_fillseq_65536x4KiB"]
@@ -224,8 +224,8 @@ def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
-    for kernel in ("ring", "ring1", "ring64", "lane64", "lane32", "wave"):
-        monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+    for kernel in ("ring", "wave"):
+        force("decoder", kernel)
         out = batch.decode_slots(c.len)
         st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
         batch.decode(comp, out, st)
@@ -234,17 +234,13 @@ def test_decode_lane_kernel_c2_full_size(gpu, digests, monkeypatch):
         assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"]), kernel
 
 
-@pytest.mark.parametrize("kernel", ["wave", "group64", "group32", "group16"])
-def test_encode_kernel_variants(gpu, vectors, digests, kernel, monkeypatch):
-    # Every encode kernel (forced through LGS_ENCODE_KERNEL) against the
-    # reference's bytes: all golden inputs in one batch (the group kernels
-    # take batches of blocks <= 4608 B; larger batches fall back), then the
-    # full C1 corpus on the device.
-    monkeypatch.setenv("LGS_ENCODE_KERNEL", kernel)
+def test_encode_small_batch_and_c1(gpu, vectors, digests):
+    # All golden inputs of <= 4 608 B in one batch, then the full C1 corpus
+    # on the device, against the reference's bytes.
     small = [v for v in vectors if v.kind == 0 and len(v.a) <= 4608]
     outs = gpu.encode_batch_host([v.a for v in small])
     for v, o in zip(small, outs):
-        assert o == v.b, (kernel, v.name)
+        assert o == v.b, v.name
     import torch
     from lcdb_amd import batch
     d = digests["C1_fillseq_1024x4KiB"]
@@ -253,18 +249,17 @@ def test_encode_kernel_variants(gpu, vectors, digests, kernel, monkeypatch):
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
     torch.cuda.synchronize()
-    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"]), kernel
+    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"])
 
 
-@pytest.mark.parametrize("kernel", ["ring", "ring1", "ring64"])
-def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, monkeypatch, kernel):
+def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
     # slots at odd offsets (flushes that are not line aligned, byte-exact
     # block ends next to the neighbouring block).
     import torch
     from lcdb_amd import batch
-    monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+    force("decoder", "ring")
     d = digests["C3_mixed"]
     c = corpus.mixed()
     raw = batch.upload(c)
@@ -319,11 +314,11 @@ def _runahead_stream(want: int, copy_frac: float) -> bytes:
 
 
 @pytest.mark.parametrize("kernel", [None, "ring"])
-def test_decode_in_place_runahead(gpu, kernel, monkeypatch):
+def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
     if kernel:
-        monkeypatch.setenv("LGS_DECODE_KERNEL", kernel)
+        force("decoder", kernel)
     ref = oracle.best()
     for want in (4000, 4600, 16000, 16800, 60000, 66000):
         streams = []
@@ -339,7 +334,7 @@ def test_decode_in_place_runahead(gpu, kernel, monkeypatch):
                 assert code == gpu.LGS_ST_OK and o == exp, (want, k)
 
 
-def test_split_launch_all_classes(gpu, monkeypatch):
+def test_split_launch_all_classes(gpu, force):
     # A batch mixing every size class, large enough (>= 16 384 blocks) that
     # the 4 KiB class goes to the ring decoder: the launch is sorted into
     # classes on the device, each class in its own kernel.  Compressed bytes
@@ -364,7 +359,7 @@ def test_split_launch_all_classes(gpu, monkeypatch):
     host = batch.to_host(comp)
     for k in list(range(0, c.n, 97)) + list(range(c.n - 100, c.n)):
         assert host.block(k) == ref.encode(c.block(k)), k
-    monkeypatch.setenv("LGS_NO_SPLIT", "1")
+    force("split", "0")
     comp2 = batch.encode_slots(raw)
     batch.encode(raw, comp2)
     torch.cuda.synchronize()

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # A/B: run bench.py once per environment setting, e.g.
-#   tools/bench_variants.sh LGS_ENCODE_KERNEL=wave LGS_ENCODE_KERNEL=group32
+#   tools/bench_variants.sh LGS_DECODE_KERNEL=ring LGS_DECODE_KERNEL=wave
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out

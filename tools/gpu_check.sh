@@ -3,7 +3,8 @@
 # Each GPU step has its own time limit.  An ordinary test failure (pytest
 # exit 1) does not stop the session; a crash, abort, signal or time limit
 # (exit >= 2) ends it before anything else touches the GPU.
-#   usage: tools/gpu_check.sh [tests] [smoke] [bench] [prof]   (default: all)
+#   usage: tools/gpu_check.sh [tests] [smoke] [bench] [prof] [latency] [pmc:TAG]
+#          (default: tests smoke bench prof)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -28,6 +29,8 @@ for s in $steps; do
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
              --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pipelined ;;
+    latency) run latency 600 python tools/bench_dropin_latency.py ;;
+    pmc:*) run "pmc_${s#pmc:}" 900 bash tools/profile.sh "${s#pmc:}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
