@@ -163,6 +163,7 @@ struct Ctx {
   size_t d_cap = 0;
   uint8_t* h_buf = nullptr; // pinned
   size_t h_cap = 0;
+  uint8_t* h_dev = nullptr; // a drop-in slot's pinned arena as the device sees it
   bool fixed = false;       // a drop-in slot: arenas never grow
 };
 
@@ -192,6 +193,8 @@ int call_device(int* dev) {
   if (*dev < 0 || *dev >= 64) return fail(LGS_ENODEV, "device %d out of range", *dev);
   return LGS_OK;
 }
+
+constexpr size_t kSlotDev = 64 << 10;   // a drop-in slot's device arena
 
 size_t env_size(const char* name, size_t dflt, size_t lo, size_t hi) {
   const char* e = getenv(name);
@@ -285,12 +288,20 @@ class CtxPool {
     LGS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     if (fixed_cap_) {
       c->fixed = true;
-      if (hipMalloc(&c->d_buf, fixed_cap_) != hipSuccess)
-        return fail(LGS_ENOMEM, "hipMalloc(%zu) failed", fixed_cap_);
-      c->d_cap = fixed_cap_;
-      if (hipHostMalloc(&c->h_buf, fixed_cap_, hipHostMallocDefault) != hipSuccess)
+      // Device memory only for the per-item arrays of an over-slot decode
+      // (in-slot calls work in the mapped pinned arena).
+      if (hipMalloc(&c->d_buf, kSlotDev) != hipSuccess)
+        return fail(LGS_ENOMEM, "hipMalloc(%zu) failed", kSlotDev);
+      c->d_cap = kSlotDev;
+      // Mapped and coherent: the kernels of an in-slot call read their input
+      // from it and write their output to it directly (no copies).
+      if (hipHostMalloc(&c->h_buf, fixed_cap_, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess)
         return fail(LGS_ENOMEM, "hipHostMalloc(%zu) failed", fixed_cap_);
       c->h_cap = fixed_cap_;
+      void* dp = nullptr;
+      LGS_HIP(hipHostGetDevicePointer(&dp, c->h_buf, 0));
+      c->h_dev = (uint8_t*)dp;
     }
     std::lock_guard<std::mutex> g(mu_);
     all_.push_back(c);
@@ -347,9 +358,9 @@ class Lease {
 
 int ctx_reserve(Ctx& c, size_t dev_bytes, size_t pin_bytes) {
   if (c.fixed) {
-    if (dev_bytes > c.d_cap || pin_bytes > c.h_cap)
-      return fail(LGS_EINTERNAL, "drop-in slot of %zu bytes, %zu needed", c.d_cap,
-                  dev_bytes > pin_bytes ? dev_bytes : pin_bytes);
+    (void)dev_bytes;                        // in-slot calls work in the pinned arena
+    if (pin_bytes > c.h_cap)
+      return fail(LGS_EINTERNAL, "drop-in slot of %zu bytes, %zu needed", c.h_cap, pin_bytes);
     return LGS_OK;
   }
   if (dev_bytes > c.d_cap) {
@@ -474,8 +485,10 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
 // leases a drop-in slot (fixed arenas of dropin_cap() bytes), so a call
 // never allocates: an input of any size goes through the slot in passes of
 // whole 64 KiB chunks, which are independent (snappy.c:370-381), and the
-// chunks' encodings are concatenated on the host as they come back.  One
-// pass = one upload, one kernel, one download, one synchronisation.
+// chunks' encodings are concatenated on the host as they come back.  The
+// slot's pinned arena is mapped into the device: a pass copies the input
+// into it, launches the kernel on it (input read and output written over
+// PCIe, no hipMemcpy) and synchronises once.
 
 // Device bytes one 64 KiB-or-less chunk takes in a pass.
 constexpr size_t kChunkIn = kChunk + 16;                         // its input
@@ -496,7 +509,7 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
   const uint32_t kmax = (uint32_t)((c.h_cap - 8 * 256) / per);
   if (kmax == 0) return fail(LGS_EINTERNAL, "drop-in slot of %zu bytes too small", c.h_cap);
   uint8_t* const h = c.h_buf;
-  uint8_t* const d = c.d_buf;
+  uint8_t* const hd = c.h_dev;
   size_t total = 0;
   for (uint32_t j0 = 0; j0 < nit; j0 += kmax) {
     const uint32_t k = nit - j0 < kmax ? nit - j0 : kmax;
@@ -521,6 +534,7 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
     LGS_TRY(ctx_reserve(c, down_end, down_end));
 
     memcpy(h + o_in, xp + at, in_bytes);
+    memset(h + o_in + in_bytes, 0, 16);
     uint64_t* ioff = (uint64_t*)(h + o_ioff);
     uint32_t* ilen = (uint32_t*)(h + o_ilen);
     uint64_t* ooff = (uint64_t*)(h + o_ooff);
@@ -534,13 +548,11 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
       oa += chunk_out(ilen[j]);
       hdr[j] = j0 + j == 0 ? n : 0xffffffffu;                    // snappy.c:368
     }
-    LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
-    EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
-                 (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen),
-                 (const uint32_t*)(d + o_hdr), nullptr, k, nullptr};
+    (void)up_end;
+    EncodeArgs a{hd, (const uint64_t*)(hd + o_ioff), (const uint32_t*)(hd + o_ilen), hd,
+                 (const uint64_t*)(hd + o_ooff), (uint32_t*)(hd + o_olen),
+                 (const uint32_t*)(hd + o_hdr), nullptr, k, nullptr};
     LGS_HIP(launch_encode(a, k == 1 ? ilen[0] : kChunk, c.stream));
-    LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, down_end - o_olen, hipMemcpyDeviceToHost,
-                           c.stream));
     LGS_HIP(hipStreamSynchronize(c.stream));
     const uint32_t* olen = (const uint32_t*)(h + o_olen);
     for (uint32_t j = 0; j < k; ++j) {
@@ -604,21 +616,20 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   const size_t o_out = L.take((size_t)want + 16);
   const size_t down_end = L.at;
   if (down_end <= c.h_cap) {
-    // In the slot: one upload, one kernel, one download (status, length and
-    // the bounded output together), one synchronisation.
-    uint8_t* const d = c.d_buf;
+    // In the slot: the kernel reads the stream from the mapped pinned arena
+    // and writes status, length and output there; one synchronisation.
+    uint8_t* const hd = c.h_dev;
+    (void)up_end;
     memcpy(h + o_in, xp, n);
+    memset(h + o_in + n, 0, 16);
     *(uint64_t*)(h + o_ioff) = o_in;
     *(uint32_t*)(h + o_ilen) = n;
     *(uint64_t*)(h + o_ooff) = o_out;
     *(uint32_t*)(h + o_ocap) = want;
-    LGS_HIP(hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, c.stream));
-    DecodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
-                 (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap),
-                 (uint32_t*)(d + o_olen), d + o_st, nullptr, 1, nullptr};
+    DecodeArgs a{hd, (const uint64_t*)(hd + o_ioff), (const uint32_t*)(hd + o_ilen), hd,
+                 (const uint64_t*)(hd + o_ooff), (const uint32_t*)(hd + o_ocap),
+                 (uint32_t*)(hd + o_olen), hd + o_st, nullptr, 1, nullptr};
     LGS_HIP(launch_decode(a, want, c.stream));
-    LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, down_end - o_st, hipMemcpyDeviceToHost,
-                           c.stream));
     LGS_HIP(hipStreamSynchronize(c.stream));
     const uint8_t st = h[o_st];
     if (st == LGS_ST_OK) memcpy(zp, h + o_out, want);
