@@ -22,8 +22,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "liblcdb_gpu_snappy.so")
 CORPUS_LIB = os.path.join(PKG, "libcorpus.so")
 
-HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip", "lgs_table.hip",
-               "lgs_bloom.hip", "lgs_table_index.cpp"]
+HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip",
+               "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp"]
 HIP_HEADERS = ["lgs_device.h", "lgs_launch.h"]
 ARCH = "gfx950"
 

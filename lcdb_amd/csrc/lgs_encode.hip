@@ -496,6 +496,13 @@ static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
 }
 
 constexpr uint32_t kEncCap0 = 4608;
+
+// The <= 4 608-byte class.  (Two blocks per wave in lockstep, half a wave
+// each, was byte-exact and slower: 1.83 against 1.21 ms on C2 -- see
+// DESIGN.md 4.1.)
+static hipError_t launch_encode_small(const EncodeArgs& a, hipStream_t s) {
+  return launch_encode_cls<kEncCap0, 1>(a, s);
+}
 constexpr uint32_t kEncCap1 = 16896;
 constexpr uint32_t kEncCap2 = 65536;
 
@@ -503,7 +510,7 @@ constexpr uint32_t kEncCap2 = 65536;
 // Blocks longer than 64 KiB are encoded chunk by chunk by their wave.
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  if (max_in <= kEncCap0) return launch_encode_cls<kEncCap0, 1>(a, s);
+  if (max_in <= kEncCap0) return launch_encode_small(a, s);
   if (a.index || a.n < kSplitMinBlocks || !options().split) {
     if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
     return launch_encode_cls<kEncCap2, 1>(a, s);
@@ -522,7 +529,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
           hipSuccess)
     return e;
   c.index = list; c.count = cnt;
-  if ((e = launch_encode_cls<kEncCap0, 1>(c, s)) != hipSuccess) return e;
+  if ((e = launch_encode_small(c, s)) != hipSuccess) return e;
   c.index = list + a.n; c.count = cnt + 1;
   if ((e = launch_encode_cls<kEncCap1, 1>(c, s)) != hipSuccess) return e;
   c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;

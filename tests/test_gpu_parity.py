@@ -237,10 +237,14 @@ def test_decode_kernels_c2_full_size(gpu, digests, force):
 def test_encode_small_batch_and_c1(gpu, vectors, digests):
     # All golden inputs of <= 4 608 B in one batch, then the full C1 corpus
     # on the device, against the reference's bytes.
+    kernel = "wave"
     small = [v for v in vectors if v.kind == 0 and len(v.a) <= 4608]
     outs = gpu.encode_batch_host([v.a for v in small])
     for v, o in zip(small, outs):
-        assert o == v.b, v.name
+        assert o == v.b, (kernel, v.name)
+    # odd counts and single blocks (a wave's second half idle)
+    for k in (1, 3):
+        assert gpu.encode_batch_host([v.a for v in small[:k]]) == [v.b for v in small[:k]]
     import torch
     from lcdb_amd import batch
     d = digests["C1_fillseq_1024x4KiB"]
@@ -249,7 +253,42 @@ def test_encode_small_batch_and_c1(gpu, vectors, digests):
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
     torch.cuda.synchronize()
+    assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"]), kernel
+
+
+def test_encode_c2_and_random(gpu, digests):
+    # The encoder on the full C2 corpus, then on random, zero, periodic and
+    # short inputs of every length class in one batch.
+    import random
+    import torch
+    from lcdb_amd import batch
+    d = digests["C2_fillseq_65536x4KiB"]
+    c = corpus.fillseq(65536)
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    torch.cuda.synchronize()
     assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"])
+    rng = random.Random(3)
+    blocks = []
+    for k in range(2001):
+        n = rng.choice([rng.randrange(0, 20), rng.randrange(20, 600), rng.randrange(600, 4609)])
+        kind = k % 4
+        if kind == 0:
+            b = bytes(rng.randrange(256) for _ in range(n))
+        elif kind == 1:
+            b = bytes(n)
+        elif kind == 2:
+            unit = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 70)))
+            b = (unit * (n // len(unit) + 1))[:n]
+        else:
+            alpha = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 4)))
+            b = bytes(rng.choice(alpha) for _ in range(n))
+        blocks.append(b)
+    outs = gpu.encode_batch_host(blocks)
+    ref = oracle.best()
+    for b, o in zip(blocks, outs):
+        assert o == ref.encode(b)
 
 
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force):
