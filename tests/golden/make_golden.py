@@ -230,6 +230,46 @@ def main() -> None:
     print(f"{len(vecs)} vectors, {os.path.getsize(VECTORS)} bytes")
 
 
+C5_ENTRIES = 32768000      # db_bench fillseq entries -> a 2.0 GiB .ldb
+
+
+def c5_table() -> dict:
+    """BASELINE config 5: the .ldb lcdb's own src/builder.c writes for
+    C5_ENTRIES fillseq entries with lcdb's own snappy.c (build_table.cpu,
+    oracle/lcdb.mk), pinned by size and SHA-256; plus its index block, which
+    at this size is tens of MiB (the multi-chunk drop-in encode, snappy.c:
+    370-374, and an over-slot decode on re-open, builder.c:99)."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "_ref", "lcdb", "build_table.cpu")
+    with tempfile.TemporaryDirectory() as tmp:
+        r = subprocess.run([exe, os.path.join(tmp, "db"), str(C5_ENTRIES), "4096"],
+                           capture_output=True, text=True, check=True)
+        assert "rc=0" in r.stdout, r.stdout
+        path = os.path.join(tmp, "db", "000001.ldb")
+        h = hashlib.sha256()
+        with open(path, "rb") as f:
+            for piece in iter(lambda: f.read(1 << 24), b""):
+                h.update(piece)
+            size = f.tell()
+            f.seek(size - 48)
+            foot = f.read(48)
+    vals, i = [], 0
+    for _ in range(4):                       # footer: metaindex + index handles
+        v = sh = 0
+        while True:
+            c = foot[i]
+            i += 1
+            v |= (c & 0x7F) << sh
+            sh += 7
+            if c < 0x80:
+                break
+        vals.append(v)
+    return {"entries": C5_ENTRIES, "block_size": 4096, "file_size": size,
+            "sha256": h.hexdigest(), "index_block_offset": vals[2],
+            "index_block_stored_bytes": vals[3]}
+
+
 def make_digests(ref) -> None:
     """Digests of the BASELINE.json corpora (reference outputs).
 
@@ -259,6 +299,7 @@ def make_digests(ref) -> None:
         "C4_fillseq_1048576x4KiB": digest(corpus.fillseq(1048576), concat=False),
         "ramp_1MiB": {"raw_bytes": 1 << 20, "comp_bytes": len(ramp),
                       "comp_sha256": hashlib.sha256(ramp).hexdigest()},
+        "C5_table_2GiB": c5_table(),
         "_generator": "tests/golden/make_golden.py with oracle/_ref/libref_snappy.so "
                       "(lcdb src/util/snappy.c compiled unmodified)",
     }

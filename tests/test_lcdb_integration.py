@@ -10,8 +10,11 @@ i.e. decodes every block) and compare the files byte for byte.
 from __future__ import annotations
 
 import filecmp
+import hashlib
+import json
 import os
 import subprocess
+import time
 
 import pytest
 
@@ -63,3 +66,46 @@ def test_build_table_gpu_identical_to_cpu(gpu, tmp_path, entries, block_size):
         outs[kind] = d / "000001.ldb"
     assert os.path.getsize(outs["cpu"]) > 0
     assert filecmp.cmp(outs["cpu"], outs["gpu"], shallow=False)
+
+
+@pytest.mark.gpu
+def test_c5_2gib_table_through_gpu_dropin(gpu, tmp_path, digests):
+    """BASELINE config 5 at its stated size: src/builder.c writes a 2.0 GiB
+    .ldb (32 768 000 fillseq entries, ~915 000 data blocks, a 34 MB index
+    block = 527 chunks of 64 KiB) through the drop-in, re-opens it through
+    the table cache and iterates it (builder.c:99, every block decoded,
+    the index block through the over-slot path); the file must equal the one
+    lcdb's own codec writes (size + SHA-256 pinned in digests.json by
+    tests/golden/make_golden.py from build_table.cpu).  The build takes
+    minutes, so progress goes to gpurun_out/c5_progress.log."""
+    d = digests["C5_table_2GiB"]
+    exe = _bin("build_table.gpu")
+    out = tmp_path / "gpu"
+    prog_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(prog_dir, exist_ok=True)
+    progress = os.path.join(prog_dir, "c5_progress.log")
+    env = dict(os.environ, TEST_TMPDIR=str(tmp_path))
+    t0 = time.time()
+    p = subprocess.Popen([exe, str(out), str(d["entries"]), str(d["block_size"])], cwd=tmp_path,
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    f = out / "000001.ldb"
+    with open(progress, "a") as log:
+        while p.poll() is None:
+            time.sleep(10)
+            size = f.stat().st_size if f.exists() else 0
+            log.write(f"{time.time() - t0:6.0f} s  build_table.gpu: {size} bytes written\n")
+            log.flush()
+            if time.time() - t0 > 1500:
+                p.kill()
+    stdout, stderr = p.communicate()
+    wall = time.time() - t0
+    assert p.returncode == 0 and "rc=0" in stdout, (stdout, stderr[-2000:])
+    assert f.stat().st_size == d["file_size"]
+    h = hashlib.sha256()
+    with open(f, "rb") as fh:
+        for piece in iter(lambda: fh.read(1 << 24), b""):
+            h.update(piece)
+    assert h.hexdigest() == d["sha256"]
+    with open(os.path.join(prog_dir, "c5_result.json"), "w") as fh:
+        json.dump({"entries": d["entries"], "file_size": d["file_size"], "sha256_ok": True,
+                   "build_and_verify_seconds": round(wall, 1)}, fh)

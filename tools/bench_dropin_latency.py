@@ -84,7 +84,7 @@ def main():
 
     # lcdb's t-db, unchanged, linked both ways (oracle/lcdb.mk).
     bindir = os.path.join(ROOT, "oracle", "_ref", "lcdb")
-    for kind in ("cpu", "gpu"):
+    for kind in (() if os.environ.get("NO_TDB") else ("cpu", "gpu")):
         exe = os.path.join(bindir, f"t-db.{kind}")
         if not os.path.exists(exe):
             continue
