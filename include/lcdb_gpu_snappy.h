@@ -312,6 +312,13 @@ int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
    LGS_EINVAL for an unknown name or value. */
 int lgs_set_option(const char *name, const char *value);
 
+/* HBM yardstick, not part of the codec: copies `bytes` (a multiple of 16)
+   from d_src to d_dst (both 16-byte aligned device pointers) with a
+   16-bytes-per-lane streaming kernel, asynchronously on `stream`.  bench.py
+   times it to report the device's achievable HBM rate beside the 8 TB/s
+   spec peak. */
+int lgs_hbm_copy_dev(void *d_dst, const void *d_src, size_t bytes, void *stream);
+
 int lgs_device_count(void);
 int lgs_set_device(int device);  /* device used by the calling thread */
 const char *lgs_last_error(void);

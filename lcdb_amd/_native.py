@@ -65,6 +65,7 @@ _SIGS = {
     "lgs_dropin_footprint": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]),
     "lgs_set_option": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "lgs_hbm_copy_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "lgs_device_count": (C.c_int, []),
     "lgs_set_device": (C.c_int, [C.c_int]),
     "lgs_last_error": (C.c_char_p, []),

@@ -567,6 +567,10 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
   return LGS_OK;
 }
 
+// The largest output an in-slot decode produces: the wave decoder's biggest
+// LDS class (lgs_decode.hip kDecCap2).
+constexpr uint32_t kInSlotDecodeMax = 66048;
+
 // Host-side reference rejects, from the header and the stream length only
 // (snappy.c:201-341): with m stream bytes after a header of `want`,
 //   * want == 0: the reference accepts exactly when m == 0 (every tag either
@@ -615,9 +619,11 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   const size_t o_olen = L.take(4);
   const size_t o_out = L.take((size_t)want + 16);
   const size_t down_end = L.at;
-  if (down_end <= c.h_cap) {
+  if (down_end <= c.h_cap && want <= kInSlotDecodeMax) {
     // In the slot: the kernel reads the stream from the mapped pinned arena
     // and writes status, length and output there; one synchronisation.
+    // (Outputs over the LDS classes decode straight against global memory,
+    // one fenced round trip per copy: those take device memory below.)
     uint8_t* const hd = c.h_dev;
     (void)up_end;
     memcpy(h + o_in, xp, n);
@@ -636,9 +642,10 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
     *ok = st == LGS_ST_OK;
     return LGS_OK;
   }
-  // Larger than the slot (multi-MiB index blocks): device memory for this
-  // call only, the stream uploaded straight from the caller's (pageable)
-  // buffer, and the output downloaded into zp only once the status says ok.
+  // Larger than the slot or than the LDS classes (multi-MiB index blocks):
+  // device memory for this call only, the stream uploaded straight from the
+  // caller's (pageable) buffer, and the output downloaded into zp only once
+  // the status says ok.
   uint8_t* big = nullptr;
   const size_t big_bytes = align_up((size_t)n + 16, 256) + align_up((size_t)want + 16, 256);
   if (hipMalloc(&big, big_bytes) != hipSuccess)
@@ -934,6 +941,15 @@ int lgs_crc32c_batch_dev(const uint8_t* d_in, const uint64_t* d_in_off, const ui
   if (n == 0) return LGS_OK;
   if (!d_in || !d_in_off || !d_in_len || !d_crc) return fail(LGS_EINVAL, "NULL argument");
   LGS_HIP(launch_crc(d_in, d_in_off, d_in_len, d_type, masked, d_crc, n, (hipStream_t)stream));
+  return LGS_OK;
+}
+
+int lgs_hbm_copy_dev(void* d_dst, const void* d_src, size_t bytes, void* stream) {
+  if (bytes == 0) return LGS_OK;
+  if (!d_dst || !d_src) return fail(LGS_EINVAL, "NULL argument");
+  if (((uintptr_t)d_dst | (uintptr_t)d_src | bytes) & 15)
+    return fail(LGS_EINVAL, "hbm copy needs 16-byte aligned pointers and length");
+  LGS_HIP(launch_hbm_copy(d_dst, d_src, bytes, (hipStream_t)stream));
   return LGS_OK;
 }
 

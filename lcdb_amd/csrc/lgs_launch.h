@@ -143,6 +143,10 @@ hipError_t launch_filter_block_match(const uint8_t* blk, uint64_t n, const uint6
                                      const uint32_t* key_len, uint32_t trim, uint8_t* match,
                                      uint32_t nq, hipStream_t s);
 
+// ---- HBM copy probe (lgs_probe.hip; bench yardstick, not the codec) ----
+// dst/src 16-byte aligned, bytes a multiple of 16.
+hipError_t launch_hbm_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 // Host runtime (lgs_api.cpp): record msg as lgs_last_error(); returns code.
 int set_error(int code, const char* msg);
 

@@ -403,3 +403,20 @@ def test_split_launch_all_classes(gpu, force):
     batch.encode(raw, comp2)
     torch.cuda.synchronize()
     assert batch.digest(comp2) == batch.digest(comp)
+
+
+def test_hbm_copy_probe_exact_and_rejects_misaligned(gpu):
+    # The bench's yardstick copy: full tiles, a ragged tail, and the
+    # alignment contract of lgs_hbm_copy_dev.
+    import torch
+    from lcdb_amd import _native
+    lib = _native.lib()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for nbytes in (16, 16 * 1023, (16 << 10) * 5 + 48, 3 << 20):
+        src = torch.randint(0, 256, (nbytes + 32,), dtype=torch.uint8, generator=g).cuda()
+        dst = torch.zeros_like(src)
+        assert lib.lgs_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), nbytes, None) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dst[:nbytes], src[:nbytes]), nbytes
+        assert int(dst[nbytes:].count_nonzero()) == 0, nbytes   # nothing past the end
+    assert lib.lgs_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), 24, None) != 0

@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit.  An ordinary test failure (pytest
 # exit 1) does not stop the session; a crash, abort, signal or time limit
 # (exit >= 2) ends it before anything else touches the GPU.
-#   usage: tools/gpu_check.sh [tests] [smoke] [bench] [prof] [latency] [pmc:TAG]
+#   usage: tools/gpu_check.sh [tests] [smoke] [bench] [prof] [latency] [pmc:TAG] [traffic:TAG]
 #          (default: tests smoke bench prof)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -31,6 +31,9 @@ for s in $steps; do
              --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pipelined ;;
     latency) run latency 600 python tools/bench_dropin_latency.py ;;
     pmc:*) run "pmc_${s#pmc:}" 900 bash tools/profile.sh "${s#pmc:}" ;;
+    # CPU only: profiles/traffic_latest.json from that PMC run, so a later
+    # bench step in the same session reports it (copy it back from the log)
+    traffic:*) run "traffic_${s#traffic:}" 120 python tools/traffic_json.py "gpurun_out/prof_${s#traffic:}" "${s#traffic:}" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
