@@ -63,16 +63,17 @@ def _run(cmd: list[str]) -> None:
     subprocess.run(cmd, check=True)
 
 
-def build_hip(force: bool = False, extra: list[str] | None = None) -> str:
+def build_hip(force: bool = False, extra: list[str] | None = None, out: str = LIB) -> str:
+    """The codec library; `out` / `extra` make probe builds (tools/probe_ab.py)."""
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [
         os.path.join(ROOT, "include", "lcdb_gpu_snappy.h")]
-    if force or _stale(LIB, deps):
-        tmp = LIB + ".tmp"
+    if force or _stale(out, deps):
+        tmp = out + ".tmp"
         _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
               "-Wall", "-Wextra", "-pthread", *srcs, "-o", tmp, *(extra or [])])
-        os.replace(tmp, LIB)
-    return LIB
+        os.replace(tmp, out)
+    return out
 
 
 def build_corpus(force: bool = False) -> str:

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""A/B timing of probe builds of the codec library on C2 (timing only).
+
+usage: python tools/probe_ab.py LIB [LIB ...]
+Each LIB (a .so built from the same sources with a probe macro, e.g.
+-DLGS_PROBE_ALIGNED_RING) runs in its own process: C2 encode and decode,
+3 warm-up + 20 timed launches each, HIP events on the launch stream.
+Probe builds may produce wrong bytes by design; only the statuses are
+checked (a probe must not change the control flow).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib: str) -> None:
+    sys.path.insert(0, ROOT)
+    import lcdb_amd.build as b
+    b.LIB = os.path.abspath(lib)
+    import numpy as np
+    import torch
+    from lcdb_amd import batch, corpus
+    c = corpus.fillseq(65536)
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    out = batch.decode_slots(c.len)
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream()
+    res = {"lib": os.path.basename(lib)}
+    for name, fn in (("encode", lambda: batch.encode(raw, comp, s)),
+                     ("decode", lambda: batch.decode(comp, out, st, s))):
+        ts = []
+        for k in range(23):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            fn()
+            e1.record(s)
+            e1.synchronize()
+            if k >= 3:
+                ts.append(e0.elapsed_time(e1) * 1e3)
+        res[name + "_us"] = float(np.mean(ts))
+        res[name + "_GiBps"] = c.raw_bytes / (res[name + "_us"] * 1e-6) / 2**30
+    res["status_ok"] = bool((st == 1).all())
+    print(json.dumps(res), flush=True)
+
+
+def main() -> None:
+    if len(sys.argv) > 2 and sys.argv[1] == "--child":
+        child(sys.argv[2])
+        return
+    for lib in sys.argv[1:]:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib],
+                           capture_output=True, text=True, timeout=300)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        print(line[-1] if line else f"{lib}: rc={r.returncode} {r.stderr[-800:]}", flush=True)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()
