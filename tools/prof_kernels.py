@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run the encode / decode kernels on a resident corpus, for rocprofv3.
 
-usage: python tools/prof_kernels.py [--blocks N] [--iters K] [--which encode,decode]
+usage: python tools/prof_kernels.py [--blocks N] [--iters K] [--which encode,decode] [--lib SO]
 Every launch is preceded by a sync so per-dispatch counters are clean.
 """
 from __future__ import annotations
@@ -12,18 +12,21 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-import torch  # noqa: E402
-
-from lcdb_amd import batch, corpus  # noqa: E402
 
 
 def main() -> None:
     p = argparse.ArgumentParser()
+    p.add_argument("--lib", default=None, help="a probe build of the codec library")
     p.add_argument("--blocks", type=int, default=65536)
     p.add_argument("--block-size", type=int, default=4096)
     p.add_argument("--iters", type=int, default=3)
     p.add_argument("--which", default="encode,decode")
     a = p.parse_args()
+    if a.lib:
+        import lcdb_amd.build as b
+        b.LIB = os.path.abspath(a.lib)
+    import torch
+    from lcdb_amd import batch, corpus
     which = a.which.split(",")
     c = corpus.fillseq(a.blocks, block_size=a.block_size)
     raw = batch.upload(c)

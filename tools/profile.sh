@@ -28,6 +28,7 @@ want sqB && pass sqB --pmc SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INS
 want tcp && pass tcp --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr
 want lds && pass lds --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE
 want lds2 && pass lds2 --pmc SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE
+want occ && pass occ --pmc MeanOccupancyPerCU
 want fetch && pass fetch --pmc FETCH_SIZE
 want write && pass write --pmc WRITE_SIZE
 exit 0
