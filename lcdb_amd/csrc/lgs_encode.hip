@@ -258,7 +258,7 @@ constexpr uint32_t kSink = kTableCap;
 // at a time are emitted lane-parallel (flush_ops), a few VALU per op instead
 // of one 64-lane pass.  (The per-op pass measured 176 against 213 GiB/s.)
 __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
-                                 const OutSlot& o, uint32_t op0, uint32_t off0, uint32_t off1) {
+                                 const OutSlot& o, uint32_t op0, uint32_t e0, uint32_t e1) {
   const uint32_t lane = lane_id();
   const uint32_t pi = 63 - lane;                      // probe index in the batch
   const uint32_t last = n - kMargin;                  // snappy.c:106
@@ -296,7 +296,7 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
   // scalar work on every trip.)
   for (;;) {
     const uint32_t v = kv + pi;
-    uint32_t o0 = off0, o1 = off1;                  // search probe pi - 2 (kv == 0)
+    uint32_t o0 = e0, o1 = e1;                      // kv == 0: see encode_kernel
     bool in_tab = true;
     if (kv != 0) {                                  // other batches: later schedule
       const uint32_t kk = v - 2;                    // (wraps for v < 2: unused)
@@ -311,11 +311,9 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
       __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
     }
     const bool isA = v == 0, isB = v == 1;
-    const bool valid = v < 2 || (in_tab && start + o1 <= last);  // snappy.c:143
+    const bool valid = in_tab && start + o1 <= last;              // snappy.c:143
     const uint64_t vmask = ballot(valid);
-    const uint32_t ps = valid ? start + o0 : 0;
-    const uint32_t pab = isA ? at - 1 : at;
-    const uint32_t p = v < 2 ? pab : ps;
+    const uint32_t p = valid ? start + o0 : 0;
 
     const uint64_t xw = lds_ld64(x, p);                           // bytes p .. p+7
     const uint32_t xv = (uint32_t)xw;
@@ -357,7 +355,9 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     // bytes at..at+6 against a zero-extended 4-byte load.
     const bool eq = xv == yv;
     const bool hi0 = ((uint32_t)(xw >> 32) & 0xffffffu) == 0;
-    const bool mt = isA ? false : (isB ? (eq & hi0) : eq);
+    // (Bitwise, not ?: -- as a select chain on v the compiler lowers it
+    // to a divergent switch.)
+    const bool mt = eq & !isA & (!isB | hi0);
     const uint64_t mm = ballot((pi < ncut) & mt) & vmask;
     const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
     // snappy.c:148, :175, :179; a group's first probe defers to its second
@@ -442,9 +442,14 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
   // Probe offsets of search probes pi - 2 (the batch right after a copy,
-  // whose lanes pi = 0, 1 are the re-probe), kept in registers.
+  // whose lanes pi = 0, 1 are the re-probe), kept in registers.  Relative
+  // to that batch's start = at + 1 the re-probe's positions are A = at - 1
+  // (offset -2) and B = at (-1), and both are always in bounds (the batch
+  // runs only while at < last): offset 0 for their bound check.
   const uint32_t pk = (63 - lane) >= 2 ? 61 - lane : 0;
   const uint32_t off0 = kProbe.off[pk], off1 = kProbe.off[pk + 1];
+  const uint32_t e0 = lane == 63 ? 0xfffffffeu : (lane == 62 ? 0xffffffffu : off0);
+  const uint32_t e1 = lane >= 62 ? 0u : off1;
   // Settle these loads now: otherwise the compiler cannot prove them done
   // inside the batch loop and waits vmcnt(0) there -- on every batch, behind
   // every pending output store.
@@ -477,7 +482,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint8_t* x = &s_in[wv][sh];
     order();
     if (clen >= kMinBlock) {
-      op = encode_chunk(x, clen, &s_tab[wv][0], o, op, off0, off1);
+      op = encode_chunk(x, clen, &s_tab[wv][0], o, op, e0, e1);
     } else {
       op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
