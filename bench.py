@@ -194,8 +194,14 @@ def main(argv=None) -> int:
 
 def run(a, rank: int, world: int, local: int, dist) -> None:
     import torch
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # One GPU per rank; with fewer visible GPUs than local ranks (a rehearsal
+    # of the N > 1 path on a smaller box) ranks share devices round-robin and
+    # the line says so -- such a value is not an N-GPU measurement.
+    ndev = torch.cuda.device_count()
+    dev_index = local % ndev if ndev else local
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    shared = ndev > 0 and world > ndev
 
     from lcdb_amd import batch, corpus, shard, snappy  # noqa: F401  (loads the HIP library)
     from lcdb_amd.build import kernel_sources_sha
@@ -366,6 +372,9 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
                        "ratio": comp_bytes / raw_bytes,
                        "partition": "round-robin block g -> rank g % N, no collective",
                        "process_group": "gloo (barrier, max-over-ranks, parity gather)",
+                       "devices": ("%d ranks SHARE %d visible GPU(s): a rehearsal, not an "
+                                   "N-GPU measurement" % (world, ndev)) if shared
+                                  else "one GPU per rank",
                        "copies_rotated": a.copies},
             "encode_GiBps": raw_bytes * world / (enc_ms * 1e-3) / 2**30,
             "decode_GiBps": raw_bytes * world / (dec_ms * 1e-3) / 2**30,
