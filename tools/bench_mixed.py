@@ -22,7 +22,11 @@ def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=32, help="x (512/128/32 blocks per half-class)")
     p.add_argument("--iters", type=int, default=10)
+    p.add_argument("--lib", default=None, help="a probe build of the codec library")
     a = p.parse_args()
+    if a.lib:
+        import lcdb_amd.build as b
+        b.LIB = os.path.abspath(a.lib)
 
     import numpy as np
     import torch
