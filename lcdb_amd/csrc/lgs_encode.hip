@@ -221,6 +221,14 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
   return op + total;
 }
 
+// snappy.c:138-143's probe schedule in closed form (skip += skip >> 5 from
+// 32: steps of 1 to probe 32, 2 to 48, 3 to 59, 4 to 67); equal to
+// kProbe.off[k] for k <= 67 (the table serves longer searches).
+__device__ __forceinline__ uint32_t probe_off(uint32_t k) {
+  return k + (k > 32 ? k - 32 : 0u) + (k > 48 ? k - 48 : 0u) + (k > 59 ? k - 59 : 0u);
+}
+constexpr uint32_t kProbeClosed = 67;
+
 // Index of the scratch slot every table / lane-id array carries past its
 // 2048 real entries: lanes that must not touch a real entry write there
 // instead of branching around the store (keeps the batch free of exec-mask
@@ -300,15 +308,20 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     bool in_tab = true;
     if (kv != 0) {                                  // other batches: later schedule
       const uint32_t kk = v - 2;                    // (wraps for v < 2: unused)
-      in_tab = kk < kProbeTab;
-      const uint32_t kc = in_tab ? kk : kProbeTab - 1;
-      o0 = kProbe.off[kc];
-      o1 = kProbe.off[kc + 1];
-      // Wait for these two loads here, on the rare path.  Left to the
-      // compiler, the wait lands where the paths merge as vmcnt(0) -- and
-      // vmcnt also counts the output stores, so every batch would stall
-      // until the previous copy's bytes had reached memory.
-      __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+      if (kv + 62 <= kProbeClosed) {                // a chunk's first batch: no load
+        o0 = probe_off(kk);
+        o1 = probe_off(kk + 1);
+      } else {
+        in_tab = kk < kProbeTab;
+        const uint32_t kc = in_tab ? kk : kProbeTab - 1;
+        o0 = kProbe.off[kc];
+        o1 = kProbe.off[kc + 1];
+        // Wait for these two loads here, on the rare path.  Left to the
+        // compiler, the wait lands where the paths merge as vmcnt(0) -- and
+        // vmcnt also counts the output stores, so every batch would stall
+        // until the previous copy's bytes had reached memory.
+        __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
+      }
     }
     const bool isA = v == 0, isB = v == 1;
     const bool valid = in_tab && start + o1 <= last;              // snappy.c:143
@@ -421,6 +434,37 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
   return op;
 }
 
+// Offsets, relative to the batch's start = at + 1, of each lane's probe in
+// the batch right after a copy: lane 63 is the re-probe's A (at - 1), lane 62
+// its B (at), lane l < 62 search probe 61 - l; e1 is the offset of the probe
+// after it (the bound check of snappy.c:143; A and B always pass it, the
+// batch runs only while at < last).
+__device__ __forceinline__ void post_copy_offsets(uint32_t lane, uint32_t* e0, uint32_t* e1) {
+  const uint32_t pk = (63 - lane) >= 2 ? 61 - lane : 0;
+  *e0 = lane == 63 ? 0xfffffffeu : (lane == 62 ? 0xffffffffu : probe_off(pk));
+  *e1 = lane >= 62 ? 0u : probe_off(pk + 1);
+}
+
+// varint32 header hv (coding.h:140-167) at the slot's start, unless hv is
+// 0xffffffff (a later chunk of a > 64 KiB block).  Returns its length.
+__device__ __forceinline__ uint32_t emit_header(const OutSlot& o, uint32_t hv) {
+  if (hv == 0xffffffffu) return 0;
+  const uint32_t lane = lane_id();
+  const uint32_t hl = hv < (1u << 7) ? 1 : hv < (1u << 14) ? 2 : hv < (1u << 21) ? 3
+                    : hv < (1u << 28) ? 4 : 5;
+  if (lane < hl) {
+    uint32_t b = (hv >> (7 * lane)) & 0x7fu;
+    if (lane + 1 < hl) b |= 0x80u;
+    o.put(0, lane, b);
+  }
+  return hl;
+}
+
+__device__ __forceinline__ OutSlot out_slot(uint8_t* out, uint64_t off, uint32_t len) {
+  return OutSlot{__builtin_amdgcn_make_buffer_rsrc(out + off, 0, (int)(32 + len + len / 6),
+                                                   0x00020000)};
+}
+
 // Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
 // its varint32 length (snappy.c:368).  Otherwise hdr[i] is the varint value
 // to prefix, or 0xffffffff for none (a later chunk of a > 64 KiB block).
@@ -446,33 +490,14 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   // to that batch's start = at + 1 the re-probe's positions are A = at - 1
   // (offset -2) and B = at (-1), and both are always in bounds (the batch
   // runs only while at < last): offset 0 for their bound check.
-  const uint32_t pk = (63 - lane) >= 2 ? 61 - lane : 0;
-  const uint32_t off0 = kProbe.off[pk], off1 = kProbe.off[pk + 1];
-  const uint32_t e0 = lane == 63 ? 0xfffffffeu : (lane == 62 ? 0xffffffffu : off0);
-  const uint32_t e1 = lane >= 62 ? 0u : off1;
-  // Settle these loads now: otherwise the compiler cannot prove them done
-  // inside the batch loop and waits vmcnt(0) there -- on every batch, behind
-  // every pending output store.
-  __builtin_amdgcn_s_waitcnt(0x0f70);                             // vmcnt(0)
+  uint32_t e0, e1;
+  post_copy_offsets(lane, &e0, &e1);
 
   const uint32_t len = uni(in_len[i]);
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
-  const OutSlot o{__builtin_amdgcn_make_buffer_rsrc(out + uni64(out_off[i]), 0,
-                                                    (int)(32 + len + len / 6), 0x00020000)};
+  const OutSlot o = out_slot(out, uni64(out_off[i]), len);
 
-  // varint32 header, coding.h:140-167.
-  const uint32_t hv = uni(hdr ? hdr[i] : len);
-  uint32_t op = 0;
-  if (hv != 0xffffffffu) {
-    const uint32_t hl = hv < (1u << 7) ? 1 : hv < (1u << 14) ? 2 : hv < (1u << 21) ? 3
-                      : hv < (1u << 28) ? 4 : 5;
-    if (lane < hl) {
-      uint32_t b = (hv >> (7 * lane)) & 0x7fu;
-      if (lane + 1 < hl) b |= 0x80u;
-      o.put(0, lane, b);
-    }
-    op = hl;
-  }
+  uint32_t op = emit_header(o, uni(hdr ? hdr[i] : len));
 
   // snappy.c:370-381: independent 64 KiB chunks, a short tail as a literal.
   // (IN_CAP >= min(len, 65536) is guaranteed by the launcher.)
@@ -506,6 +531,11 @@ constexpr uint32_t kEncCap0 = 4608;
 // each, was byte-exact and slower: 1.83 against 1.21 ms on C2 -- see
 // DESIGN.md 4.1.)
 static hipError_t launch_encode_small(const EncodeArgs& a, hipStream_t s) {
+  // (Persistent waves that prefetch the next block into registers while
+  // parsing one were byte-exact and 15 % slower, 1 286 against 1 118 us on
+  // C2: a wave's wait for its next block also drains its previous block's
+  // output stores (vmcnt counts both), and a static partition of blocks over
+  // waves balances worse than dispatching one-wave workgroups.)
   return launch_encode_cls<kEncCap0, 1>(a, s);
 }
 constexpr uint32_t kEncCap1 = 16896;
