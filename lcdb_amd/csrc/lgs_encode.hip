@@ -224,10 +224,17 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
 // snappy.c:138-143's probe schedule in closed form (skip += skip >> 5 from
 // 32: steps of 1 to probe 32, 2 to 48, 3 to 59, 4 to 67); equal to
 // kProbe.off[k] for k <= 67 (the table serves longer searches).
-__device__ __forceinline__ uint32_t probe_off(uint32_t k) {
+__host__ __device__ constexpr uint32_t probe_off(uint32_t k) {
   return k + (k > 32 ? k - 32 : 0u) + (k > 48 ? k - 48 : 0u) + (k > 59 ? k - 59 : 0u);
 }
 constexpr uint32_t kProbeClosed = 67;
+constexpr bool probe_off_matches_table() {
+  constexpr ProbeTable t;
+  for (uint32_t k = 0; k <= kProbeClosed; ++k)
+    if (probe_off(k) != t.off[k]) return false;
+  return true;
+}
+static_assert(probe_off_matches_table(), "closed-form probe schedule != snappy.c:138-143");
 
 // Index of the scratch slot every table / lane-id array carries past its
 // 2048 real entries: lanes that must not touch a real entry write there
