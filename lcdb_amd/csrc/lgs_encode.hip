@@ -283,7 +283,10 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     tsize <<= 1;
     --shift;
   }
-  for (uint32_t e = lane; e < tsize; e += kWave) tab[e] = 0;   // snappy.c:129
+  // snappy.c:129, 16 bytes (8 entries) per lane and store: tsize >= 256
+  // entries is a whole number of 64-lane rows.
+  for (uint32_t e = lane; e < tsize / 8; e += kWave)
+    reinterpret_cast<u32x4*>(tab)[e] = u32x4{0, 0, 0, 0};
   order();
 
   uint32_t op = op0;     // output cursor (byte offset in the slot)
