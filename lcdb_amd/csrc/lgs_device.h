@@ -109,6 +109,15 @@ __device__ __forceinline__ uint64_t lds_ld64(const uint8_t* base, uint32_t at) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// 16 bytes starting at `at` (bytes at..at+15): five aligned dwords.
+__device__ __forceinline__ u32x4 lds_ld128(const uint8_t* base, uint32_t at) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));
+  const uint32_t a = w[0], b = w[1], c = w[2], d = w[3], e = w[4];
+  const uint32_t s = at & 3u;
+  return u32x4{__builtin_amdgcn_alignbyte(b, a, s), __builtin_amdgcn_alignbyte(c, b, s),
+               __builtin_amdgcn_alignbyte(d, c, s), __builtin_amdgcn_alignbyte(e, d, s)};
+}
+
 // Copy `len` bytes global->LDS: the LDS image keeps the source's alignment
 // mod 16 (byte k of the source lands at lds[(src & 15) + k]) so that every
 // lane moves one aligned 16-byte granule.  Returns the LDS shift (src & 15).

@@ -39,9 +39,20 @@ struct OutSlot {
   __device__ void put(uint32_t soff, uint32_t voff, uint32_t v) const {
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)voff, (int)soff, 0);
   }
-  // Four bytes at any byte offset (gfx950 buffer stores need no alignment).
+  // 2, 4, 8 or 16 bytes at any byte offset (gfx950 buffer stores need no
+  // alignment).
+  __device__ void put2(uint32_t soff, uint32_t voff, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, (int)voff, (int)soff, 0);
+  }
   __device__ void put4(uint32_t soff, uint32_t voff, uint32_t v) const {
     __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, 0);
+  }
+  __device__ void put8(uint32_t soff, uint32_t voff, uint32_t lo, uint32_t hi) const {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, r, (int)voff, (int)soff, 0);
+  }
+  __device__ void put16(uint32_t soff, uint32_t voff, u32x4 v) const {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, (int)soff, 0);
   }
 };
 
@@ -121,11 +132,10 @@ __device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uin
 // being the literal from the previous op's end (lit0 for op 0) to its copy
 // start, then the copy (snappy.c:156, :166).  Every lane sizes its op
 // (snappy.c:53-102), a wave scan places it, then
-//   1. literal bytes, 4 per trip from LDS with one unaligned dword store,
-//      each lane its own op's (a trip may write up to 3 bytes past a
-//      literal: into that op's tags or the next op's first byte, both
-//      rewritten in step 3; four byte stores per trip measured 3 % slower
-//      in encode time);
+//   1. literal bytes, each lane its own op's: 16 bytes per trip from LDS
+//      with one unaligned 16-byte store, then the last < 16 bytes with
+//      exact-size stores (byte stores, one per byte, measured 3 % slower in
+//      encode time);
 //   2. literals over kLongLit bytes: all lanes on one op at a time;
 //   3. literal headers and copy tags; copies of 68+ bytes (several pieces,
 //      rare) through emit_copy, one op at a time.
@@ -185,13 +195,30 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
   const uint32_t lat = excl + hl;                                     // literal's first byte
   const uint32_t tat = lat + LL;                                      // copy's first tag byte
   constexpr uint32_t kOff = 0x40000000u;                              // dropped by the range check
-  // 1. short literals, lane-parallel.
+  // 1. short literals, lane-parallel: whole 16-byte pieces, then the last
+  //    < 16 bytes with one 8-, 4-, 2- and 1-byte store each (lanes that do
+  //    not need one aim it past the slot), so no byte lands past a literal.
   const uint32_t LLs = LL > kLongLit ? 0u : LL;
+  const uint32_t whole = LLs & ~15u;
 #pragma clang loop unroll(disable)
-  for (uint32_t t = 0; ballot(t < LLs); t += 4) {
-    const bool on = t < LLs;
-    const uint32_t v = lds_ld32(x, on ? lit + t : 0u);
-    o.put4(op, on ? lat + t : kOff, v);
+  for (uint32_t t = 0; ballot(t < whole); t += 16) {
+    const bool on = t < whole;
+    o.put16(op, on ? lat + t : kOff, lds_ld128(x, on ? lit + t : 0u));
+  }
+  {
+    const uint32_t rem = LLs - whole;                 // 0..15
+    u32x4 v = lds_ld128(x, LLs ? lit + whole : 0u);
+    uint32_t at = lat + whole;
+    o.put8(op, (rem & 8) ? at : kOff, v.x, v.y);
+    if (rem & 8) v = u32x4{v.z, v.w, 0, 0};
+    at += rem & 8;
+    o.put4(op, (rem & 4) ? at : kOff, v.x);
+    if (rem & 4) v.x = v.y;
+    at += rem & 4;
+    o.put2(op, (rem & 2) ? at : kOff, v.x);
+    if (rem & 2) v.x >>= 16;
+    at += rem & 2;
+    o.put(op, (rem & 1) ? at : kOff, v.x);
   }
   // 2. long literals, all lanes on one op at a time (rare).
   for (uint64_t big = ballot(LL > kLongLit); big; big &= big - 1) {
