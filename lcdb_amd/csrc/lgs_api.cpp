@@ -826,6 +826,10 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
     out_total += align_up(bound_of(in_len[i]), 16);
     if (in_len[i] > max_in) max_in = in_len[i];
   }
+  // The encodings land in bound-spaced device slots; a scan of their lengths
+  // and a pack kernel then put them end to end, so only the compressed bytes
+  // cross PCIe (C2: 153 MB instead of 316 MB of slots).  The packed region
+  // comes back into the pinned slot region, which it never exceeds.
   Layout L;
   const size_t o_in = L.take(in_total + 16);
   const size_t o_ioff = L.take(8 * (size_t)n);
@@ -833,9 +837,14 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   const size_t o_ooff = L.take(8 * (size_t)n);
   const size_t up_end = L.at;
   const size_t o_olen = L.take(4 * (size_t)n);
+  const size_t o_poff = L.take(8 * (size_t)n);
+  const size_t o_pend = L.take(8);
+  const size_t meta_end = L.at;
   const size_t o_out = L.take(out_total + 16);
   const size_t down_end = L.at;
-  LGS_TRY(ctx_reserve(c, down_end, down_end));
+  const size_t o_part = L.take(8 * scan_parts(n) + 8);          // device only
+  const size_t o_pack = L.take(out_total + 16);                 // device only
+  LGS_TRY(ctx_reserve(c, L.at, down_end));
   uint8_t* h = c.h_buf;
   uint8_t* d = c.d_buf;
   uint64_t* ioff = (uint64_t*)(h + o_ioff);
@@ -856,13 +865,22 @@ int lgs_encode_batch_host(const uint8_t* in, const uint64_t* in_off, const uint3
   EncodeArgs a{d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), d,
                (const uint64_t*)(d + o_ooff), (uint32_t*)(d + o_olen), nullptr, nullptr, n, nullptr};
   LGS_HIP(launch_encode(a, max_in, c.stream));
-  LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, down_end - o_olen, hipMemcpyDeviceToHost,
+  LGS_HIP(launch_scan(2, nullptr, (const uint32_t*)(d + o_olen), (uint64_t*)(d + o_part), 0,
+                      (uint64_t*)(d + o_poff), (uint64_t*)(d + o_pend), n, c.stream));
+  LGS_HIP(launch_pack(d, (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_olen),
+                      d + o_pack, (const uint64_t*)(d + o_poff), n, c.stream));
+  LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, meta_end - o_olen, hipMemcpyDeviceToHost,
                          c.stream));
   LGS_HIP(hipStreamSynchronize(c.stream));
+  const uint64_t packed = *(const uint64_t*)(h + o_pend);
+  if (packed > out_total) return fail(LGS_EINTERNAL, "packed encodings exceed their slots");
+  LGS_HIP(hipMemcpyAsync(h + o_out, d + o_pack, packed, hipMemcpyDeviceToHost, c.stream));
+  LGS_HIP(hipStreamSynchronize(c.stream));
   const uint32_t* olen = (const uint32_t*)(h + o_olen);
-  par_for(n, in_total, [&](uint32_t i0, uint32_t i1) {
+  const uint64_t* poff = (const uint64_t*)(h + o_poff);
+  par_for(n, packed, [&](uint32_t i0, uint32_t i1) {
     for (uint32_t i = i0; i < i1; ++i) {
-      memcpy(out + out_off[i], h + ooff[i], olen[i]);
+      memcpy(out + out_off[i], h + o_out + poff[i], olen[i]);
       out_len[i] = olen[i];
     }
   });

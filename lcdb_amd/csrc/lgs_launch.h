@@ -100,12 +100,17 @@ struct CheckArgs {
 hipError_t launch_crc(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                       const uint8_t* type, int masked, uint32_t* crc, uint32_t n, hipStream_t s);
 // Exclusive scan of per-item region sizes (mode 0: 16-aligned encode bounds;
-// mode 1: framed block sizes) into u64 offsets starting at base; *end = base
-// + total when end != null.  part: scan_parts(n) u64 of device scratch.
+// mode 1: framed block sizes; mode 2: enc_len itself) into u64 offsets
+// starting at base; *end = base + total when end != null.  part:
+// scan_parts(n) u64 of device scratch.
 size_t scan_parts(uint32_t n);
 hipError_t launch_scan(int mode, const uint32_t* raw_len, const uint32_t* enc_len, uint64_t* part,
                        uint64_t base, uint64_t* off, uint64_t* end, uint32_t n, hipStream_t s);
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s);
+// Item i's len[i] bytes from src + src_off[i] to dst + dst_off[i] (any
+// alignment; the regions do not overlap).
+hipError_t launch_pack(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
+                       uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s);
 hipError_t launch_check(const CheckArgs& a, hipStream_t s);
 hipError_t launch_merge(uint8_t* status, uint32_t* out_len, const uint8_t* dec_status,
                         const uint32_t* dec_out_len, uint32_t n, hipStream_t s);

@@ -266,13 +266,15 @@ __global__ __launch_bounds__(64 * WAVES) void crc_kernel(
 
 // ---- row 2: data-block framing ------------------------------------------
 
-// Size of item i's region in one of two layouts:
+// Size of item i's region in one of three layouts:
 //   MODE 0: encode slot, 16-byte aligned encode bound (snappy.c:354);
 //   MODE 1: framed block in the file: contents (compressed only when that
-//           saves more than 12.5 %, table_builder.c:190) + 5-byte trailer.
+//           saves more than 12.5 %, table_builder.c:190) + 5-byte trailer;
+//   MODE 2: the encoded bytes alone, packed (lgs_encode_batch_host).
 template <int MODE>
 __device__ __forceinline__ uint64_t item_size(const uint32_t* raw_len, const uint32_t* enc_len,
                                               uint32_t i) {
+  if (MODE == 2) return enc_len[i];
   const uint32_t L = raw_len[i];
   if (MODE == 0) return ((uint64_t)32 + L + L / 6 + 15) & ~15ull;
   const uint32_t e = enc_len ? enc_len[i] : 0xffffffffu;
@@ -514,17 +516,62 @@ hipError_t launch_scan(int mode, const uint32_t* raw_len, const uint32_t* enc_le
   const uint32_t np = (uint32_t)scan_parts(n);
   if (mode == 0) {
     hipLaunchKernelGGL(scan_part_kernel<0>, dim3(np), dim3(kScanT), 0, s, raw_len, enc_len, part, n);
-  } else {
+  } else if (mode == 1) {
     hipLaunchKernelGGL(scan_part_kernel<1>, dim3(np), dim3(kScanT), 0, s, raw_len, enc_len, part, n);
+  } else {
+    hipLaunchKernelGGL(scan_part_kernel<2>, dim3(np), dim3(kScanT), 0, s, raw_len, enc_len, part, n);
   }
   hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanT), 0, s, part, np);
   if (mode == 0) {
     hipLaunchKernelGGL(scan_out_kernel<0>, dim3(np), dim3(kScanT), 0, s, raw_len, enc_len, part,
                        base, off, end, n);
-  } else {
+  } else if (mode == 1) {
     hipLaunchKernelGGL(scan_out_kernel<1>, dim3(np), dim3(kScanT), 0, s, raw_len, enc_len, part,
                        base, off, end, n);
+  } else {
+    hipLaunchKernelGGL(scan_out_kernel<2>, dim3(np), dim3(kScanT), 0, s, raw_len, enc_len, part,
+                       base, off, end, n);
   }
+  return hipGetLastError();
+}
+
+// Item i's len[i] bytes from src + src_off[i] to dst + dst_off[i], one wave
+// per item: whole 16-byte destination granules with one (unaligned) 16-byte
+// load and one aligned store, the ragged ends byte by byte.
+template <uint32_t WAVES>
+__global__ __launch_bounds__(64 * WAVES) void pack_kernel(const uint8_t* __restrict__ src,
+                                                         const uint64_t* __restrict__ src_off,
+                                                         const uint32_t* __restrict__ len,
+                                                         uint8_t* __restrict__ dst,
+                                                         const uint64_t* __restrict__ dst_off,
+                                                         uint32_t n) {
+  typedef u32x4 u32x4_g __attribute__((aligned(1)));
+  for (uint32_t i = uni(blockIdx.x * WAVES + (threadIdx.x >> 6)); i < n;
+       i += gridDim.x * WAVES) {
+    const gptr<const uint8_t> s = to_global(src) + src_off[i];
+    const gptr<uint8_t> d = to_global(dst) + dst_off[i];
+    const uint32_t e = len[i];
+    const uint64_t d0 = (uint64_t)(uintptr_t)d;
+    const uint64_t g_lo = d0 & ~15ull, g_hi = (d0 + e + 15) & ~15ull;
+    for (uint64_t g = g_lo + 16ull * lane_id(); g < g_hi; g += 16ull * kWave) {
+      const int64_t k0 = (int64_t)(g - d0);
+      if (g >= d0 && g + 16 <= d0 + e) {
+        *(gptr<u32x4>)(d + k0) = *(gptr<const u32x4_g>)(s + k0);
+      } else {
+        for (uint32_t t = 0; t < 16; ++t) {
+          const int64_t k = k0 + t;
+          if (k >= 0 && k < (int64_t)e) d[k] = s[k];
+        }
+      }
+    }
+  }
+}
+
+hipError_t launch_pack(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
+                       uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_kernel<kFrameWaves>, dim3(frame_grid(pack_kernel<kFrameWaves>, n)),
+                     dim3(64 * kFrameWaves), 0, s, src, src_off, len, dst, dst_off, n);
   return hipGetLastError();
 }
 

@@ -27,7 +27,11 @@ def main() -> None:
     p = argparse.ArgumentParser()
     p.add_argument("--blocks", type=int, default=65536)
     p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--lib", default=None, help="a probe build of the codec library")
     a = p.parse_args()
+    if a.lib:
+        import lcdb_amd.build as b
+        b.LIB = os.path.abspath(a.lib)
 
     from lcdb_amd import _native, corpus  # noqa: E402
     from lcdb_amd._native import check
