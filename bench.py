@@ -73,6 +73,10 @@ def parse(argv=None) -> argparse.Namespace:
                    help="skip the 1 GiB copy that measures the achievable HBM rate")
     p.add_argument("--no-pipelined", action="store_true",
                    help="skip the extra concurrent encode||decode measurement")
+    p.add_argument("--no-c3", action="store_true",
+                   help="skip the extra C3 (mixed 4/16/64 KiB) measurement at N = 1")
+    p.add_argument("--c3-scale", type=int, default=32,
+                   help="C3 scale: 512/128/32 blocks per half-class x this")
     p.add_argument("--plan-only", action="store_true",
                    help="no GPU: launch, partition and digest-gather only (CPU tests)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -359,6 +363,14 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(c, a, hc)
 
+    # ---- extra (not `value`): BASELINE.json configs[2] on this GPU, after
+    # everything above, with its own buffers (the C2 ones are freed first).
+    c3 = None
+    if world == 1 and not a.no_c3:
+        del raws, comps, outs, stats
+        torch.cuda.empty_cache()
+        c3 = c3_mixed(a, dev, stream)
+
     if rank == 0:
         line = {
             "metric": baseline["metric"], "value": value, "unit": "GiB/s",
@@ -379,10 +391,74 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
             "encode_GiBps": raw_bytes * world / (enc_ms * 1e-3) / 2**30,
             "decode_GiBps": raw_bytes * world / (dec_ms * 1e-3) / 2**30,
             "kernels": kern, "roofline": roof, "cpu_baseline": cpu, "parity": parity,
-            "pipelined": pipelined,
+            "pipelined": pipelined, "c3": c3,
             "gen_seconds": t_gen,
         }
         print(json.dumps(line), flush=True)
+
+
+def c3_mixed(a, dev, stream) -> dict:
+    """BASELINE.json configs[2] (C3): 4/16/64 KiB blocks, half db_bench
+    fillseq, half uniform random (corpus.mixed), at --c3-scale.  Each class
+    as its own batch and the whole mix as one batch (the split launch sorts
+    it into classes on the device); HIP events on the launch stream, median
+    of 10 after 2 warm-ups; every decode round-trip checked, the mix's
+    compressed blocks diffed against the pinned reference digest."""
+    import torch
+    from lcdb_amd import batch, corpus
+    scale = a.c3_scale
+
+    def timed(fn) -> float:
+        ts = []
+        for k in range(12):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            if k >= 2:
+                ts.append(e0.elapsed_time(e1) * 1e-3)
+        return float(np.median(ts))
+
+    def one(c) -> tuple[dict, object]:
+        raw = batch.upload(c, dev)
+        comp = batch.encode_slots(raw)
+        out = batch.decode_slots(c.len, dev)
+        st = torch.zeros(c.n, dtype=torch.uint8, device=dev)
+        t_e = timed(lambda: batch.encode(raw, comp, stream))
+        t_d = timed(lambda: batch.decode(comp, out, st, stream))
+        ho = batch.to_host(out)
+        ok = bool((st == 1).all()) and np.array_equal(
+            corpus.block_digests(ho.buf, ho.off, ho.len), corpus.block_digests(c.buf, c.off, c.len))
+        rb, cb = c.raw_bytes, int(comp.len.sum(dtype=torch.int64).item())
+        hc = batch.to_host(comp)
+        del raw, out, st, comp
+        torch.cuda.empty_cache()
+        return ({"blocks": c.n, "raw_bytes": rb, "ratio": cb / rb,
+                 "encode_GiBps": rb / t_e / 2**30, "decode_GiBps": rb / t_d / 2**30,
+                 "encode_ms": t_e * 1e3, "decode_ms": t_d * 1e3, "roundtrip_ok": ok}, hc)
+
+    classes = {}
+    for bs, n in ((4096, 512), (16384, 128), (65536, 32)):
+        for kind in ("fillseq", "random"):
+            c = (corpus.fillseq(n * scale, block_size=bs, key0=bs) if kind == "fillseq"
+                 else corpus.random_blocks(n * scale, bs, seed=0x5EED + bs))
+            classes[f"{kind}_{bs // 1024}K"] = one(c)[0]
+    mix, hc = one(corpus.mixed(scale))
+    dg = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+    ref = dg.get("C3_mixed" if scale == 1 else f"C3_mixed_x{scale}")
+    ok = all(r["roundtrip_ok"] for r in classes.values()) and mix["roundtrip_ok"]
+    if ref is None:
+        parity = "round trips exact" if ok else "MISMATCH (round trip or status)"
+    else:
+        same = corpus.digest_of_digests(corpus.block_digests(hc.buf, hc.off, hc.len)) == \
+            ref["comp_dd"]
+        parity = ("round trips exact, mix's compressed blocks == reference digest"
+                  if ok and same else "MISMATCH against the reference digest")
+    return {"workload": f"C3: mixed 4/16/64 KiB, half fillseq / half random, scale {scale} "
+                        f"({mix['blocks']} blocks, {mix['raw_bytes']} B)",
+            "classes": classes, "mixed_one_launch": mix, "parity": parity,
+            "note": "extra field (BASELINE.json configs[2]), not value"}
 
 
 def achievable_copy_gbps(dev, stream) -> dict:

@@ -270,6 +270,21 @@ def c5_table() -> dict:
             "index_block_stored_bytes": vals[3]}
 
 
+def digest(ref, c: corpus.Corpus, threads: int = 8, concat: bool = True) -> dict:
+    """The reference's compressed output of corpus c, as digests."""
+    out, ooff, olen = ref.encode_batch(c.buf, c.off, c.len, threads=threads)
+    d = {"blocks": c.n, "raw_bytes": c.raw_bytes,
+         "comp_bytes": int(olen.sum(dtype=np.uint64)),
+         "raw_dd": corpus.digest_of_digests(corpus.block_digests(c.buf, c.off, c.len)),
+         "comp_dd": corpus.digest_of_digests(corpus.block_digests(out, ooff, olen))}
+    if concat:
+        h = hashlib.sha256()
+        for o, k in zip(ooff, olen):
+            h.update(memoryview(out[int(o):int(o) + int(k)]))
+        d.update(raw_sha256=c.sha256(), comp_sha256=h.hexdigest())
+    return d
+
+
 def make_digests(ref) -> None:
     """Digests of the BASELINE.json corpora (reference outputs).
 
@@ -277,26 +292,15 @@ def make_digests(ref) -> None:
     concatenated per-block SHA-256s (lcdb_amd.corpus.digest_of_digests), which
     round-robin shards reassemble without moving blocks (bench.py at N > 1).
     C4 (1 048 576 blocks, BASELINE.json configs[3]) is pinned by its _dd
-    digests only."""
-    def digest(c: corpus.Corpus, threads: int = 8, concat: bool = True) -> dict:
-        out, ooff, olen = ref.encode_batch(c.buf, c.off, c.len, threads=threads)
-        d = {"blocks": c.n, "raw_bytes": c.raw_bytes,
-             "comp_bytes": int(olen.sum(dtype=np.uint64)),
-             "raw_dd": corpus.digest_of_digests(corpus.block_digests(c.buf, c.off, c.len)),
-             "comp_dd": corpus.digest_of_digests(corpus.block_digests(out, ooff, olen))}
-        if concat:
-            h = hashlib.sha256()
-            for o, k in zip(ooff, olen):
-                h.update(memoryview(out[int(o):int(o) + int(k)]))
-            d.update(raw_sha256=c.sha256(), comp_sha256=h.hexdigest())
-        return d
+    digests only.  C3_mixed_x32 is the mix at the scale bench.py times."""
 
     ramp = ref.encode(bytes(i & 255 for i in range(1 << 20)))
     digs = {
-        "C1_fillseq_1024x4KiB": digest(corpus.fillseq(1024)),
-        "C2_fillseq_65536x4KiB": digest(corpus.fillseq(65536)),
-        "C3_mixed": digest(corpus.mixed()),
-        "C4_fillseq_1048576x4KiB": digest(corpus.fillseq(1048576), concat=False),
+        "C1_fillseq_1024x4KiB": digest(ref, corpus.fillseq(1024)),
+        "C2_fillseq_65536x4KiB": digest(ref, corpus.fillseq(65536)),
+        "C3_mixed": digest(ref, corpus.mixed()),
+        "C3_mixed_x32": digest(ref, corpus.mixed(32)),
+        "C4_fillseq_1048576x4KiB": digest(ref, corpus.fillseq(1048576), concat=False),
         "ramp_1MiB": {"raw_bytes": 1 << 20, "comp_bytes": len(ramp),
                       "comp_sha256": hashlib.sha256(ramp).hexdigest()},
         "C5_table_2GiB": c5_table(),
@@ -311,5 +315,13 @@ if __name__ == "__main__":
     if "--digests-only" in sys.argv:
         import oracle
         make_digests(oracle.reference())
+    elif "--add-c3x32" in sys.argv:
+        # merge one digest into the pinned file without re-running the rest
+        import oracle
+        with open(DIGESTS) as f:
+            digs = json.load(f)
+        digs["C3_mixed_x32"] = digest(oracle.reference(), corpus.mixed(32))
+        with open(DIGESTS, "w") as f:
+            json.dump(digs, f, indent=2, sort_keys=True)
     else:
         main()

@@ -6,7 +6,9 @@ Each LIB (a .so built from the same sources with a probe macro, e.g.
 -DLGS_PROBE_ALIGNED_RING) runs in its own process: C2 encode and decode,
 3 warm-up + 20 timed launches each, HIP events on the launch stream.
 Probe builds may produce wrong bytes by design; only the statuses are
-checked (a probe must not change the control flow).
+checked (a probe must not change the control flow).  With PROBE_CHECK=1
+each library's C2 output is also checked against the pinned reference
+digest and the raw blocks (for candidate builds, not probes).
 """
 from __future__ import annotations
 
@@ -46,6 +48,14 @@ def child(lib: str) -> None:
         res[name + "_us"] = float(np.mean(ts))
         res[name + "_GiBps"] = c.raw_bytes / (res[name + "_us"] * 1e-6) / 2**30
     res["status_ok"] = bool((st == 1).all())
+    if os.environ.get("PROBE_CHECK"):
+        # a candidate (not a probe): its bytes must be the reference's
+        dg = json.load(open(os.path.join(ROOT, "tests", "golden", "digests.json")))
+        hc, ho = batch.to_host(comp), batch.to_host(out)
+        res["encode_exact"] = corpus.digest_of_digests(
+            corpus.block_digests(hc.buf, hc.off, hc.len)) == dg["C2_fillseq_65536x4KiB"]["comp_dd"]
+        res["decode_exact"] = bool(np.array_equal(corpus.block_digests(ho.buf, ho.off, ho.len),
+                                                  corpus.block_digests(c.buf, c.off, c.len)))
     print(json.dumps(res), flush=True)
 
 
