@@ -184,7 +184,10 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
   uint32_t apos = sh + hlen;                        // absolute LDS offset of the next tag
   const uint32_t aend = sh + slen;
   uint32_t made = 0;
-  uint32_t pend = (uint32_t)((int32_t)aend + gap) + kWave + lane, pv = 0;
+  // The stream's never-consumed pad: the deferred write's target until the
+  // first op.
+  const uint32_t pad = (uint32_t)((int32_t)aend + gap) + kWave + lane;
+  uint32_t pend = pad, pv = 0, res = 1;
 
   while (apos < aend) {                             // snappy.c:208
     // ---- the window: lane l parses a tag at q = w + l (reads stay inside
@@ -216,41 +219,87 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
     const uint32_t fstep = (lit ? lbad : cbad) ? 0u : (lit ? lhl + llen : chl);
     const uint32_t flen = lit ? llen : clen;
     const uint32_t fx = lit ? q + lhl : (cdist | 0x80000000u);
+    // The common op -- no stream reject, a literal of <= 64 bytes or a copy
+    // with dist >= len -- is accepted by one unsigned range test on `made`:
+    // lo <= made <= hi, where made >= dist is snappy.c:323's source bound,
+    // made <= want - len is :263 / :323's length bound, and made <= gap +
+    // lim - 64 is the in-place bound below (lim: a copy's stream ends at
+    // q + step, a literal reads from fx).  Everything else (and every tag
+    // that fails the test) takes the exact path below.
+    const int32_t lim = lit ? (int32_t)fx : (int32_t)(q + fstep);
+    const int32_t hi0 = (int32_t)want - (int32_t)flen, hi1 = gap + lim - (int32_t)kWave;
+    const int32_t hmax = hi0 < hi1 ? hi0 : hi1;
+    const uint32_t lo = lit ? 0u : cdist;
+    const bool fast = (fstep != 0) & (lit ? llen <= kWave : cdist >= clen) & (hmax >= (int32_t)lo);
+    const uint32_t flo = fast ? lo : 0xffffffffu;
+    const uint32_t frng = fast ? (uint32_t)hmax - lo : 0u;
+    // The op's first source byte relative to o: a literal's in the staged
+    // stream (base == o + gap), a copy's at made - dist (made added below).
+    const uint32_t fsrc = lit ? (uint32_t)(gap + (int32_t)fx) : 0u - cdist;
+    const uint32_t fpk = (fast ? flen | (fstep << 8) : 0u) | (lit ? 0u : 0x10000u);
 
-    // ---- the serial walk over this window's tags.
+    // ---- the serial walk over this window's tags.  Both paths end in one
+    // deferred write + one read, so the read's register is never copied
+    // (a copy would wait for the read).
+    const uint32_t wend = aend - w < kWave ? aend : w + kWave;
     do {
       const uint32_t d = apos - w;
-      const uint32_t st = __builtin_amdgcn_readlane(fstep, d);
-      const uint32_t len = __builtin_amdgcn_readlane(flen, d);
-      const uint32_t x = __builtin_amdgcn_readlane(fx, d);
-      const bool cp = (x >> 31) != 0;
-      const uint32_t dist = x & 0x7fffffffu;
-      // snappy.c:263 (literal) and :323 (copy); the in-place bound (a
-      // literal reads from x, a copy's stream ends at apos + st).
-      const bool bad = (st == 0) | (len > want - made) | (cp & (made < dist));
-      const int32_t lim = cp ? (int32_t)(apos + st) : (int32_t)x;
-      const bool ahead = (int32_t)(made + kWave) - lim > gap;
-      if (bad | ahead) return bad ? 0u : 3u;
-      o[pend] = (uint8_t)pv;
-      if (!cp) {
-        if (len <= kWave) {
-          pv = base[x + lane];
-        } else {
-          for (uint32_t j = lane; j < len; j += kWave) o[made + j] = base[x + j];
-          pv = o[made + lane];
-        }
-      } else if (dist >= len) {
-        pv = o[made - dist + lane];
+      const uint32_t rlo = __builtin_amdgcn_readlane(flo, d);
+      const uint32_t rrng = __builtin_amdgcn_readlane(frng, d);
+      uint32_t len = 0, step = 0, from = 0;
+      if (made - rlo <= rrng) {
+        const uint32_t pk = __builtin_amdgcn_readlane(fpk, d);
+        const uint32_t src = __builtin_amdgcn_readlane(fsrc, d);
+        len = pk & 0xffu;
+        step = (pk >> 8) & 0xffu;
+        from = src + ((pk >> 16) ? made : 0u) + lane;
       } else {
-        pv = o[made - dist + lane % dist];          // lanes >= len: wild, overwritten later
+        step = __builtin_amdgcn_readlane(fstep, d);
+        len = __builtin_amdgcn_readlane(flen, d);
+        const uint32_t x = __builtin_amdgcn_readlane(fx, d);
+        const bool cp = (x >> 31) != 0;
+        const uint32_t dist = x & 0x7fffffffu;
+        // snappy.c:263 (literal) and :323 (copy); the in-place bound (a
+        // literal reads from x, a copy's stream ends at apos + step).
+        const bool bad = (step == 0) | (len > want - made) | (cp & (made < dist));
+        const int32_t lm = cp ? (int32_t)(apos + step) : (int32_t)x;
+        const bool ahead = (int32_t)(made + kWave) - lm > gap;
+        if (bad | ahead) {
+          // One exit per loop (no selector chains from loop-exit
+          // unification): end both walks; the tail below writes nothing
+          // that matters (a corrupt block is not flushed, a run-ahead one
+          // is decoded again from global memory into o).
+          res = bad ? 0u : 3u;
+          apos = aend;
+          step = 0;
+          len = 0;
+          from = made + lane;
+        } else if (!cp) {
+          if (len <= kWave) {
+            from = (uint32_t)gap + x + lane;                     // base[x + lane]
+          } else {
+            o[pend] = (uint8_t)pv;                               // before the piece writes
+            order();
+            for (uint32_t j = lane; j < len; j += kWave) o[made + j] = base[x + j];
+            pend = pad;                                          // the write below: harmless
+            from = made + lane;
+          }
+        } else if (dist >= len) {
+          from = made - dist + lane;
+        } else {
+          from = made - dist + lane % dist;          // lanes >= len: wild, overwritten later
+        }
       }
+      o[pend] = (uint8_t)pv;
+      pv = o[from];
       pend = made + lane;
       order();
       made += len;
-      apos += st;
-    } while (apos < aend && apos - w < kWave);
+      apos += step;
+    } while (apos < wend);
   }
   o[pend] = (uint8_t)pv;
+  if (res != 1) return res;
 
   return made == want ? 1u : 0u;                    // snappy.c:337
 }
