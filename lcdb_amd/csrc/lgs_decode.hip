@@ -190,53 +190,39 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
   uint32_t pend = pad, pv = 0, res = 1;
 
   while (apos < aend) {                             // snappy.c:208
-    // ---- the window: lane l parses a tag at q = w + l (reads stay inside
-    // the staging pad past the stream end; lanes past it are never used).
+    // ---- the window: lane l looks at the tag that would start at q = w + l
+    // (reads stay inside the staging pad past the stream end; lanes past it
+    // are never used) and decides whether it is a *common* tag: a literal
+    // with a one-byte header (<= 60 bytes) or a COPY1 / COPY2 whose bytes do
+    // not overlap (dist >= len), inside the stream.  For those it packs what
+    // the walk needs; every other tag, and every common tag that fails the
+    // walk's one test, is decoded by the exact scalar path below.
     const uint32_t w = apos;
     const uint32_t q = w + lane;
-    const uint64_t t = lds_ld64(base, q);
-    const uint32_t tag = (uint32_t)t & 0xffu;
-    const uint32_t kind = tag & 3u;
-    const uint32_t hi = (uint32_t)(t >> 8);
-    const uint32_t left = aend - q;
-    // literal, snappy.c:210-258
-    const uint32_t m0 = tag >> 2;
-    const bool ext = m0 >= 60;
-    const uint32_t extra = ext ? m0 - 59 : 0u;
-    const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
-    const uint32_t m = ext ? (hi & emask) : m0;
-    const uint32_t lhl = 1 + extra, llen = m + 1;
-    const bool lbad = (ext & (left - 1 < extra)) | (m >= 0x7fffffffu) | (llen > left - lhl);
-    // copies, snappy.c:276-320
-    const uint32_t clen = kind == 1 ? 4 + ((tag >> 2) & 7u) : 1 + (tag >> 2);
-    const uint32_t cdist = kind == 1 ? ((tag & 0xe0u) << 3) | (hi & 0xffu)
-                                     : (kind == 2 ? hi & 0xffffu : hi);
-    const uint32_t chl = kind == 1 ? 2u : (kind == 2 ? 3u : 5u);
-    const bool cbad = (left < chl) | (cdist == 0) | (cdist >= 0x80000000u);
+    const uint32_t t = lds_ld32(base, q);
+    const uint32_t tag = t & 0xffu, kind = tag & 3u, m0 = tag >> 2;
     const bool lit = kind == 0;
-    // Packed for the walk: step 0 marks a stream-only reject; a copy's
-    // distance carries bit 31 (a valid one is < 2^31).
-    const uint32_t fstep = (lit ? lbad : cbad) ? 0u : (lit ? lhl + llen : chl);
-    const uint32_t flen = lit ? llen : clen;
-    const uint32_t fx = lit ? q + lhl : (cdist | 0x80000000u);
-    // The common op -- no stream reject, a literal of <= 64 bytes or a copy
-    // with dist >= len -- is accepted by one unsigned range test on `made`:
-    // lo <= made <= hi, where made >= dist is snappy.c:323's source bound,
-    // made <= want - len is :263 / :323's length bound, and made <= gap +
-    // lim - 64 is the in-place bound below (lim: a copy's stream ends at
-    // q + step, a literal reads from fx).  Everything else (and every tag
-    // that fails the test) takes the exact path below.
-    const int32_t lim = lit ? (int32_t)fx : (int32_t)(q + fstep);
-    const int32_t hi0 = (int32_t)want - (int32_t)flen, hi1 = gap + lim - (int32_t)kWave;
+    const uint32_t len = kind == 1 ? 4 + (m0 & 7u) : m0 + 1;       // snappy.c:216, 276, 289
+    const uint32_t dist = kind == 1 ? ((tag & 0xe0u) << 3) | ((t >> 8) & 0xffu)
+                                    : (t >> 8) & 0xffffu;            // snappy.c:279, 292
+    const uint32_t step = lit ? len + 1 : kind + 1;
+    // The walk accepts the tag when lo <= made <= hmax: made >= dist is
+    // snappy.c:323's source bound, made <= want - len the length bound of
+    // :263 / :323, and made <= gap + lim - 64 the in-place bound (a copy's
+    // stream ends at q + step, a literal reads from q + 1).
+    const int32_t lim = (int32_t)q + (int32_t)(lit ? 1u : step);
+    const int32_t hi0 = (int32_t)want - (int32_t)len, hi1 = gap + lim - (int32_t)kWave;
     const int32_t hmax = hi0 < hi1 ? hi0 : hi1;
-    const uint32_t lo = lit ? 0u : cdist;
-    const bool fast = (fstep != 0) & (lit ? llen <= kWave : cdist >= clen) & (hmax >= (int32_t)lo);
+    const uint32_t lo = lit ? 0u : dist;
+    const bool common = (lit ? m0 < 60 : (kind != 3) & (dist >= len) & (dist != 0)) &
+                        (step <= aend - q);
+    const bool fast = common & (hmax >= (int32_t)lo);
     const uint32_t flo = fast ? lo : 0xffffffffu;
-    const uint32_t frng = fast ? (uint32_t)hmax - lo : 0u;
+    const uint32_t frng = fast ? (uint32_t)(hmax - (int32_t)lo) : 0u;
     // The op's first source byte relative to o: a literal's in the staged
     // stream (base == o + gap), a copy's at made - dist (made added below).
-    const uint32_t fsrc = lit ? (uint32_t)(gap + (int32_t)fx) : 0u - cdist;
-    const uint32_t fpk = (fast ? flen | (fstep << 8) : 0u) | (lit ? 0u : 0x10000u);
+    const uint32_t fsrc = lit ? (uint32_t)(gap + (int32_t)q + 1) : 0u - dist;
+    const uint32_t fpk = len | (step << 8) | (lit ? 0u : 0x10000u);
 
     // ---- the serial walk over this window's tags.  Both paths end in one
     // deferred write + one read, so the read's register is never copied
@@ -246,24 +232,43 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
       const uint32_t d = apos - w;
       const uint32_t rlo = __builtin_amdgcn_readlane(flo, d);
       const uint32_t rrng = __builtin_amdgcn_readlane(frng, d);
-      uint32_t len = 0, step = 0, from = 0;
+      uint32_t n = 0, adv = 0, from = 0;
       if (made - rlo <= rrng) {
         const uint32_t pk = __builtin_amdgcn_readlane(fpk, d);
         const uint32_t src = __builtin_amdgcn_readlane(fsrc, d);
-        len = pk & 0xffu;
-        step = (pk >> 8) & 0xffu;
+        n = pk & 0xffu;
+        adv = (pk >> 8) & 0xffu;
         from = src + ((pk >> 16) ? made : 0u) + lane;
       } else {
-        step = __builtin_amdgcn_readlane(fstep, d);
-        len = __builtin_amdgcn_readlane(flen, d);
-        const uint32_t x = __builtin_amdgcn_readlane(fx, d);
-        const bool cp = (x >> 31) != 0;
-        const uint32_t dist = x & 0x7fffffffu;
-        // snappy.c:263 (literal) and :323 (copy); the in-place bound (a
-        // literal reads from x, a copy's stream ends at apos + step).
-        const bool bad = (step == 0) | (len > want - made) | (cp & (made < dist));
-        const int32_t lm = cp ? (int32_t)(apos + step) : (int32_t)x;
-        const bool ahead = (int32_t)(made + kWave) - lm > gap;
+        // The exact tag step of snappy.c:210-324, on the SALU.
+        const uint64_t tv = uni64(lds_ld64(base, apos));
+        const uint32_t tg = (uint32_t)tv & 0xffu, kd = tg & 3u;
+        const uint32_t hi = (uint32_t)(tv >> 8), left = aend - apos;
+        bool bad = false;
+        uint32_t x = 0, ds = 0;
+        int32_t lm = 0;
+        if (kd == 0) {                              // literal, snappy.c:210-273
+          uint32_t m = tg >> 2, hl = 1;
+          if (m >= 60) {
+            const uint32_t extra = m - 59;          // 1..4 length bytes
+            bad = left - 1 < extra;
+            m = extra == 4 ? hi : (hi & ((1u << (8 * (extra & 3u))) - 1u));
+            hl += extra;
+          }
+          n = m + 1;
+          bad = bad || m >= 0x7fffffffu || n > left - hl || n > want - made;   // :258, :263
+          x = apos + hl;
+          adv = hl + n;
+          lm = (int32_t)x;
+        } else {                                    // copies, snappy.c:276-324
+          const uint32_t chl = kd == 1 ? 2u : (kd == 2 ? 3u : 5u);
+          n = kd == 1 ? 4 + ((tg >> 2) & 7u) : 1 + (tg >> 2);
+          ds = kd == 1 ? ((tg & 0xe0u) << 3) | (hi & 0xffu) : (kd == 2 ? hi & 0xffffu : hi);
+          bad = left < chl || ds == 0 || ds >= 0x80000000u || made < ds || n > want - made;
+          adv = chl;
+          lm = (int32_t)(apos + chl);
+        }
+        const bool ahead = (int32_t)(made + kWave) - lm > gap;   // the in-place bound
         if (bad | ahead) {
           // One exit per loop (no selector chains from loop-exit
           // unification): end both walks; the tail below writes nothing
@@ -271,31 +276,31 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
           // is decoded again from global memory into o).
           res = bad ? 0u : 3u;
           apos = aend;
-          step = 0;
-          len = 0;
+          adv = 0;
+          n = 0;
           from = made + lane;
-        } else if (!cp) {
-          if (len <= kWave) {
+        } else if (kd == 0) {
+          if (n <= kWave) {
             from = (uint32_t)gap + x + lane;                     // base[x + lane]
           } else {
             o[pend] = (uint8_t)pv;                               // before the piece writes
             order();
-            for (uint32_t j = lane; j < len; j += kWave) o[made + j] = base[x + j];
+            for (uint32_t j = lane; j < n; j += kWave) o[made + j] = base[x + j];
             pend = pad;                                          // the write below: harmless
             from = made + lane;
           }
-        } else if (dist >= len) {
-          from = made - dist + lane;
+        } else if (ds >= n) {
+          from = made - ds + lane;
         } else {
-          from = made - dist + lane % dist;          // lanes >= len: wild, overwritten later
+          from = made - ds + lane % ds;             // lanes >= n: wild, overwritten later
         }
       }
       o[pend] = (uint8_t)pv;
       pv = o[from];
       pend = made + lane;
       order();
-      made += len;
-      apos += step;
+      made += n;
+      apos += adv;
     } while (apos < wend);
   }
   o[pend] = (uint8_t)pv;
@@ -934,9 +939,14 @@ constexpr uint32_t kDecCap0 = 4608;    // fillseq "4 KiB" blocks (max 4208 B)
 constexpr uint32_t kDecCap1 = 16896;   // 16 KiB class
 constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoot)
 
-// Batches of at least this many blocks go to the lane-per-block kernel
-// (one wave per 64 blocks still fills the chip).
-constexpr uint32_t kLaneMinBlocks = 16384;
+// Batches of at least this many blocks go to the lane-per-block ring
+// kernel, smaller ones to the wave-per-block kernel.  Measured on 4 KiB
+// fillseq blocks (tools/sweep_decoders.py, round 2): ring 292 / wave 268 us
+// at 32 768 blocks, 316 / 328 at 40 960 (the ring's time is one generation
+// of its trips until the chip is full, the wave kernel's grows with the
+// batch).  On incompressible blocks the wave kernel wins at every size
+// (98 against 163 us at 49 152), but a launch does not know the ratio.
+constexpr uint32_t kLaneMinBlocks = 36864;
 
 // ---------------------------------------------------------------------------
 // Mixed-size batches.  One launch sized for its largest block runs every

@@ -374,7 +374,7 @@ def test_decode_in_place_runahead(gpu, kernel, force):
 
 
 def test_split_launch_all_classes(gpu, force):
-    # A batch mixing every size class, large enough (>= 16 384 blocks) that
+    # A batch mixing every size class, large enough (>= 36 864 blocks) that
     # the 4 KiB class goes to the ring decoder: the launch is sorted into
     # classes on the device, each class in its own kernel.  Compressed bytes
     # equal the reference's (oracle, per block) and the unsplit launch's;
@@ -382,7 +382,7 @@ def test_split_launch_all_classes(gpu, force):
     import torch
     from lcdb_amd import batch
     ref = oracle.best()
-    c = corpus.concat(corpus.fillseq(16000), corpus.random_blocks(400, 4096),
+    c = corpus.concat(corpus.fillseq(36600), corpus.random_blocks(400, 4096),
                       corpus.fillseq(40, block_size=16384), corpus.random_blocks(30, 16384),
                       corpus.fillseq(12, block_size=65536), corpus.random_blocks(6, 65536),
                       corpus.fillseq(3, block_size=100000), corpus.random_blocks(2, 70000))
