@@ -28,7 +28,7 @@ for s in $steps; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-             --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pipelined ;;
+             --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-pipelined --no-c3 ;;
     latency) run latency 600 python tools/bench_dropin_latency.py ;;
     pmc:*) run "pmc_${s#pmc:}" 900 bash tools/profile.sh "${s#pmc:}" ;;
     # CPU only: profiles/traffic_latest.json from that PMC run, so a later
