@@ -420,3 +420,67 @@ def test_hbm_copy_probe_exact_and_rejects_misaligned(gpu):
         assert torch.equal(dst[:nbytes], src[:nbytes]), nbytes
         assert int(dst[nbytes:].count_nonzero()) == 0, nbytes   # nothing past the end
     assert lib.lgs_hbm_copy_dev(dst.data_ptr(), src.data_ptr(), 24, None) != 0
+
+
+def _lit(b: bytes) -> bytes:
+    # literal tag, snappy.c:53-73 header forms (1-3 length bytes here)
+    n = len(b) - 1
+    if n < 60:
+        return bytes([n << 2]) + b
+    if n < 256:
+        return bytes([60 << 2, n]) + b
+    if n < 65536:
+        return bytes([61 << 2, n & 255, n >> 8]) + b
+    return bytes([62 << 2, n & 255, (n >> 8) & 255, n >> 16]) + b
+
+
+def _copy2(length: int, dist: int) -> bytes:
+    return bytes([((length - 1) << 2) | 2, dist & 255, dist >> 8])
+
+
+def test_decode_wide_far_copies_long_literals_and_rejects(gpu):
+    # Outputs over the 16 KiB class go to the wide decoder (a 32 KiB output
+    # ring flushed to HBM, a 4 KiB stream ring refilled 2 KiB at a time).
+    # Hand-made streams put copies beyond the ring (dist > 32 704, read back
+    # from HBM), literals across many refills and flushes, and every kind of
+    # reject at different depths; real 64 KiB / 100 KB / 300 KB blocks and
+    # their corruptions follow.  Each against the reference's accept/reject
+    # bit and bytes.
+    import random
+    rng = random.Random(11)
+    ref = oracle.best()
+    rnd = lambda n: bytes(rng.randrange(256) for _ in range(n))  # noqa: E731
+    body = (_lit(rnd(40000)) + _copy2(64, 40000) + _copy2(64, 33000) + _copy2(20, 32705)
+            + _lit(rnd(100)) + _copy2(60, 40200) + bytes([1 | (6 << 2) | (3 << 5), 0x10])
+            + _lit(rnd(70000)) + _copy2(64, 65535) + _copy2(7, 3) + _copy2(64, 1))
+    made = 40000 + 64 + 64 + 20 + 100 + 60 + 10 + 70000 + 64 + 7 + 64
+    good = _varint(made) + body
+    streams = [good,
+               good[:-1],                                    # truncated tag
+               good[:len(good) // 2],                        # truncated literal
+               _varint(made + 1) + body,                     # stream ends short of want
+               _varint(made - 1) + body,                     # op past want (snappy.c:323)
+               _varint(40100) + _lit(rnd(40000)) + _copy2(64, 40001),   # dist > produced
+               _varint(40100) + _lit(rnd(40000)) + bytes([2, 0, 0]),    # dist == 0
+               _varint(70000) + _lit(rnd(70000))[:-5],       # literal past the stream
+               _varint(5) + bytes([63 << 2, 1, 0, 0, 0]) + b"abcde"]     # 4-byte length
+    for bs, n in ((65536, 3), (100000, 2), (300000, 1)):
+        c = corpus.fillseq(n, block_size=bs, key0=bs)
+        r = corpus.random_blocks(n, bs, seed=bs)
+        for blk in [c.block(k) for k in range(c.n)] + [r.block(k) for k in range(r.n)]:
+            s = ref.encode(blk)
+            streams += [s, s[:-3]]
+            for _ in range(4):
+                k = rng.randrange(1, len(s))
+                streams.append(s[:k] + bytes([rng.randrange(256)]) + s[k + 1:])
+    caps = [1 << 19] * len(streams)
+    res, st = gpu.decode_batch_host(streams, caps)
+    oks = 0
+    for k, (s, o, code) in enumerate(zip(streams, res, st)):
+        exp = ref.decode(s)
+        if exp is None:
+            assert code == gpu.LGS_ST_CORRUPT, k
+        else:
+            assert code == gpu.LGS_ST_OK and o == exp, k
+            oks += 1
+    assert oks >= 13
