@@ -491,17 +491,9 @@ __device__ __forceinline__ uint8_t gl_byte(const uint8_t* p) {
 // bound; a copy reaching further back than the ring (dist > 32 704) reads
 // the flushed output from HBM after its stores have drained.
 // ---------------------------------------------------------------------------
-namespace wide {
-constexpr uint32_t kOut = 32768;            // output ring
-constexpr uint32_t kIn = 4096;              // input ring
-constexpr uint32_t kMirror = 80;            // stream bytes kIn.. mirror 0..79
-constexpr uint32_t kBuf = kOut + kIn + kMirror + kWave;   // + a pad for harmless writes
-constexpr uint32_t kPad = kOut + kIn + kMirror;
-constexpr uint32_t kRefill = 2048;          // stream bytes per refill (2 granules a lane)
-constexpr uint32_t kFlushAt = 8192;         // pending output that triggers a flush
-constexpr uint32_t kFar = kOut - kWave;     // copies up to this distance read the ring
-}  // namespace wide
 
+// OUT / IN: the output and input ring sizes (powers of two, IN >= 2048).
+template <uint32_t OUT, uint32_t IN>
 __global__ __launch_bounds__(64) void decode_wide_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -509,7 +501,20 @@ __global__ __launch_bounds__(64) void decode_wide_kernel(
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
     const uint32_t* __restrict__ index, uint32_t n,
     const uint32_t* __restrict__ count) {
-  using namespace wide;
+  constexpr uint32_t kOut = OUT;             // output ring
+  constexpr uint32_t kIn = IN;               // input ring
+  constexpr uint32_t kMirror = 80;           // stream bytes kIn.. mirror ring offsets 0..79
+  constexpr uint32_t kBuf = kOut + kIn + kMirror + kWave;   // + a pad for harmless writes
+  constexpr uint32_t kPad = kOut + kIn + kMirror;
+  constexpr uint32_t kRefill = kIn / 2;      // stream bytes per refill
+  constexpr uint32_t kGran = kRefill / 1024; // 16-byte granules per lane and refill
+  // Pending output that triggers a flush.  A window makes <= 4 KiB, so the
+  // unflushed bytes stay under kFlushAt + 4 160 < kOut - 64 (the pending
+  // write's wild lanes never reach an unflushed byte), and a far copy's
+  // source (dist > kFar) ends below F.
+  constexpr uint32_t kFlushAt = kOut / 4;
+  constexpr uint32_t kFar = kOut - kWave;    // copies up to this distance read the ring
+  static_assert(kFlushAt + 4224 <= kOut && (kGran == 1 || kGran == 2), "ring sizes");
   __shared__ __attribute__((aligned(16))) uint8_t sb[kBuf];
   uint8_t* const ib = sb + kOut;            // input ring
 
@@ -551,15 +556,17 @@ __global__ __launch_bounds__(64) void decode_wide_kernel(
   auto prefetch = [&]() {
     const uint32_t c0 = staged + 16 * lane, c1 = c0 + 1024;
     if (c0 < slen) pf0 = ld16(src + c0);
-    if (c1 < slen) pf1 = ld16(src + c1);
+    if (kGran == 2 && c1 < slen) pf1 = ld16(src + c1);
   };
   auto land = [&]() {       // the prefetched chunk into the ring, then the next prefetch
     __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
     const uint32_t r0 = (staged + 16 * lane) & (kIn - 1), r1 = (r0 + 1024) & (kIn - 1);
     *reinterpret_cast<u32x4*>(ib + r0) = pf0;
-    *reinterpret_cast<u32x4*>(ib + r1) = pf1;
     if (r0 < kMirror) *reinterpret_cast<u32x4*>(ib + kIn + r0) = pf0;
-    if (r1 < kMirror) *reinterpret_cast<u32x4*>(ib + kIn + r1) = pf1;
+    if (kGran == 2) {
+      *reinterpret_cast<u32x4*>(ib + r1) = pf1;
+      if (r1 < kMirror) *reinterpret_cast<u32x4*>(ib + kIn + r1) = pf1;
+    }
     order();
     staged += kRefill;
     prefetch();
@@ -1193,10 +1200,18 @@ Scratch::Scratch(size_t bytes, hipStream_t s) : s_(s) {
 
 // Outputs over the 16 KiB class: the wide decoder (any size; the 64 KiB class
 // decoded 70 GiB/s in decode_kernel<66048>, two waves per CU).
+template <uint32_t OUT, uint32_t IN>
 static hipError_t launch_decode_wide(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(decode_wide_kernel, dim3(a.n), dim3(64), 0, s, a.in, a.in_off, a.in_len,
-                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n, a.count);
+  hipLaunchKernelGGL((decode_wide_kernel<OUT, IN>), dim3(a.n), dim3(64), 0, s, a.in, a.in_off,
+                     a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n,
+                     a.count);
   return hipGetLastError();
+}
+// The 16 KiB class stays in decode_kernel's in-place image (18 KB, eight
+// waves per CU): the rings at 8 KiB + 2 KiB (10.4 KB, fourteen waves) were
+// slower on C3's 16 KiB classes (fillseq 212 -> 204 GiB/s, random 838 -> 690).
+static hipError_t launch_decode_mid(const DecodeArgs& a, hipStream_t s) {
+  return launch_decode_cls<kDecCap1, 1>(a, s);
 }
 
 static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
@@ -1211,14 +1226,14 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
   c.index = list; c.count = cnt;
   LGS_TRY((a.n >= kLaneMinBlocks ? launch_decode_ring(c, s) : launch_decode_cls<kDecCap0, 1>(c, s)));
   c.index = list + a.n; c.count = cnt + 1;
-  LGS_TRY((launch_decode_cls<kDecCap1, 1>(c, s)));
+  LGS_TRY(launch_decode_mid(c, s));
   if (max_out > kDecCap1) {            // (classes above max_out are empty)
     c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
-    LGS_TRY(launch_decode_wide(c, s));
+    LGS_TRY((launch_decode_wide<32768, 4096>(c, s)));
   }
   if (max_out > kDecCap2) {
     c.index = list + 3 * (size_t)a.n; c.count = cnt + 3;
-    LGS_TRY(launch_decode_wide(c, s));
+    LGS_TRY((launch_decode_wide<32768, 4096>(c, s)));
   }
   return scratch.release();
 }
@@ -1232,8 +1247,8 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))
     return launch_decode_ring(a, s);
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
-  if (max_out <= kDecCap1) return launch_decode_cls<kDecCap1, 1>(a, s);
-  return launch_decode_wide(a, s);
+  if (max_out <= kDecCap1) return launch_decode_mid(a, s);
+  return launch_decode_wide<32768, 4096>(a, s);
 }
 
 }  // namespace lgs
