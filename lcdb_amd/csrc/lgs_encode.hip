@@ -56,10 +56,104 @@ struct OutSlot {
   }
 };
 
+// Where encode_chunk reads its chunk.  LdsIn: the whole chunk staged in LDS
+// (every class up to 16 KiB, and C2).  WinIn: the 64 KiB class's window, a
+// W-byte LDS ring of the chunk with the chunk in HBM behind it, so four
+// waves fit a CU instead of two.  lcdb's 2 048-entry table keeps candidates
+// from anywhere in the chunk, but on fillseq only ~40 of a 64 KiB block's
+// 26 600 probes find one more than 28 000 bytes back (tools: the age
+// simulation in DESIGN.md), so reads outside the ring take a slow path: a
+// wave-uniform test, then global loads for the lanes that need them.
+struct LdsIn {
+  static constexpr bool kWin = false;
+  const uint8_t* x;
+  __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(x, p); }
+  __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(x, p); }
+  __device__ uint32_t byte(uint32_t p) const { return x[p]; }
+  __device__ u32x4 lit128(uint32_t p) const { return lds_ld128(x, p); }
+  __device__ uint32_t litbyte(uint32_t p) const { return x[p]; }
+  __device__ bool oow(uint32_t, uint32_t) const { return false; }
+  __device__ void ensure(uint32_t) {}
+  __device__ uint64_t g64(uint32_t) const { return 0; }
+  __device__ uint32_t g32(uint32_t) const { return 0; }
+  __device__ uint32_t gbyte(uint32_t) const { return 0; }
+};
+
+template <uint32_t W>
+struct WinIn {
+  static constexpr bool kWin = true;
+  uint8_t* ring;                 // W bytes + a 16-byte mirror of ring[0..15]
+  gptr<const uint8_t> gal;       // the chunk's first byte's 16-byte granule
+  uint32_t sh;                   // chunk start & 15: position p is u = p + sh
+  uint32_t n;                    // chunk length
+  uint32_t hu;                   // staged below u = hu (a multiple of 16); valid: u >= hu - W
+  __device__ uint32_t ri(uint32_t p) const { return (p + sh) & (W - 1); }
+  __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(ring, ri(p)); }
+  __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(ring, ri(p)); }
+  __device__ uint32_t byte(uint32_t p) const { return ring[ri(p)]; }
+  // bytes p .. p+k-1 are not in the ring
+  __device__ bool oow(uint32_t p, uint32_t k) const {
+    const uint32_t u = p + sh;
+    return (u + W < hu) | (u + k > hu);
+  }
+  // Global dword d (of the granule-aligned view), clamped to the chunk's last
+  // dword: reads never leave the granules that hold the chunk's bytes.
+  __device__ uint32_t gdw(uint32_t d) const {
+    const uint32_t last = (n + sh - 1) >> 2;
+    return *(gptr<const uint32_t>)(gal + 4 * (d < last ? d : last));
+  }
+  __device__ uint64_t g64(uint32_t p) const {
+    const uint32_t u = p + sh, d = u >> 2, b = u & 3u;
+    const uint32_t a = gdw(d), c = gdw(d + 1), e = gdw(d + 2);
+    return ((uint64_t)__builtin_amdgcn_alignbyte(e, c, b) << 32) | __builtin_amdgcn_alignbyte(c, a, b);
+  }
+  __device__ uint32_t g32(uint32_t p) const {
+    const uint32_t u = p + sh;
+    return __builtin_amdgcn_alignbyte(gdw((u >> 2) + 1), gdw(u >> 2), u & 3u);
+  }
+  __device__ uint32_t gbyte(uint32_t p) const {
+    const uint32_t u = p + sh;
+    return (gdw(u >> 2) >> (8 * (u & 3u))) & 0xffu;
+  }
+  // Emission reads literals from HBM (a literal may start anywhere behind).
+  __device__ u32x4 lit128(uint32_t p) const {
+    const uint32_t u = p + sh, d = u >> 2, b = u & 3u;
+    const uint32_t a0 = gdw(d), a1 = gdw(d + 1), a2 = gdw(d + 2), a3 = gdw(d + 3), a4 = gdw(d + 4);
+    return u32x4{__builtin_amdgcn_alignbyte(a1, a0, b), __builtin_amdgcn_alignbyte(a2, a1, b),
+                 __builtin_amdgcn_alignbyte(a3, a2, b), __builtin_amdgcn_alignbyte(a4, a3, b)};
+  }
+  __device__ uint32_t litbyte(uint32_t p) const { return gbyte(p); }
+  // Stage 4 KiB more (16-byte granules, each lane four), waiting for them.
+  __device__ void stage() {
+    const uint32_t lane = lane_id(), gend = (n + sh + 15) >> 4;
+    u32x4 v[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t g = (hu >> 4) + lane + 64 * j;
+      v[j] = g < gend ? *(gptr<const u32x4>)(gal + 16 * g) : u32x4{0, 0, 0, 0};
+    }
+    __builtin_amdgcn_s_waitcnt(0x0f70);                          // vmcnt(0)
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t r = (hu + 16 * (lane + 64 * j)) & (W - 1);
+      *reinterpret_cast<u32x4*>(ring + r) = v[j];
+      if (r < 16) *reinterpret_cast<u32x4*>(ring + W + r) = v[j];
+    }
+    order();
+    hu += 4096;
+  }
+  // Positions below P staged (as far as the chunk goes).
+  __device__ void ensure(uint32_t P) {
+    const uint32_t want = (P < n ? P : n) + sh;
+    while (hu < want) stage();
+  }
+};
+
 // snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o:
 // header (1-3 bytes) and bytes in one pass, lane j writing output byte j.
 // Returns bytes written.
-__device__ __forceinline__ uint32_t emit_literal(const OutSlot& o, uint32_t op, const uint8_t* in,
+template <class IN>
+__device__ __forceinline__ uint32_t emit_literal(const OutSlot& o, uint32_t op, const IN& in,
                                                  uint32_t from, uint32_t len) {
   const uint32_t lane = lane_id();
   const uint32_t m = len - 1;
@@ -71,7 +165,7 @@ __device__ __forceinline__ uint32_t emit_literal(const OutSlot& o, uint32_t op, 
   for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
     const uint32_t j = j0 + lane;
     // Unconditional (clamped) LDS read, then a select: no branch around it.
-    const uint32_t lb = in[from + (j >= hl ? j - hl : 0)];
+    const uint32_t lb = in.litbyte(from + (j >= hl ? j - hl : 0));
     const uint32_t v = j < hl ? (hdr >> (8 * j)) : lb;
     if (j < total) o.put(op, j, v);
   }
@@ -154,7 +248,8 @@ __device__ __forceinline__ void write_lane2(uint32_t& a, uint32_t sa, uint32_t& 
       "v_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0\n\ts_mov_b32 m0, %2"
       : "+v"(a), "+v"(b), "=&s"(keep) : "s"(sa), "s"(sb), "s"(l));
 }
-__device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, const uint8_t* x,
+template <class IN>
+__device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, const IN& x,
                                               uint32_t recA, uint32_t recB, uint32_t k,
                                               uint32_t lit0) {
   const uint32_t lane = lane_id();
@@ -203,11 +298,11 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
 #pragma clang loop unroll(disable)
   for (uint32_t t = 0; ballot(t < whole); t += 16) {
     const bool on = t < whole;
-    o.put16(op, on ? lat + t : kOff, lds_ld128(x, on ? lit + t : 0u));
+    o.put16(op, on ? lat + t : kOff, x.lit128(on ? lit + t : 0u));
   }
   {
     const uint32_t rem = LLs - whole;                 // 0..15
-    u32x4 v = lds_ld128(x, LLs ? lit + whole : 0u);
+    u32x4 v = x.lit128(LLs ? lit + whole : 0u);
     uint32_t at = lat + whole;
     o.put8(op, (rem & 8) ? at : kOff, v.x, v.y);
     if (rem & 8) v = u32x4{v.z, v.w, 0, 0};
@@ -227,7 +322,7 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
 #pragma clang loop unroll(disable)
     for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
       const uint32_t j = j0 + lane;
-      const uint32_t b = x[from + (j < len ? j : 0u)];
+      const uint32_t b = x.litbyte(from + (j < len ? j : 0u));
       o.put(op, j < len ? to + j : kOff, b);
     }
   }
@@ -301,7 +396,8 @@ constexpr uint32_t kSink = kTableCap;
 // on the spot: the op is recorded in lane registers (v_writelane) and 64 ops
 // at a time are emitted lane-parallel (flush_ops), a few VALU per op instead
 // of one 64-lane pass.  (The per-op pass measured 176 against 213 GiB/s.)
-__device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, uint16_t* tab,
+template <class IN>
+__device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* tab,
                                  const OutSlot& o, uint32_t op0, uint32_t e0, uint32_t e1) {
   const uint32_t lane = lane_id();
   const uint32_t pi = 63 - lane;                      // probe index in the batch
@@ -367,13 +463,22 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
     const uint64_t vmask = ballot(valid);
     const uint32_t p = valid ? start + o0 : 0;
 
-    const uint64_t xw = lds_ld64(x, p);                           // bytes p .. p+7
+    if constexpr (IN::kWin) x.ensure(start + lane_val(o0, 0) + 16);   // lane 0: the last probe
+    uint64_t xw = x.rd64(p);                                      // bytes p .. p+7
+    if constexpr (IN::kWin) {
+      const bool op_ = valid & x.oow(p, 8);
+      if (ballot(op_)) xw = op_ ? x.g64(p) : xw;
+    }
     const uint32_t xv = (uint32_t)xw;
     const uint32_t hh = valid ? hash32(xv, shift) : kSink;
     // The table read and the candidate's bytes do not depend on the
     // lane-id rounds below: issue them first so their LDS latency overlaps.
     const uint32_t ct = tab[hh];                                  // snappy.c:146, :177
-    uint32_t yv = lds_ld32(x, valid ? ct : 0);
+    uint32_t yv = x.rd32(valid ? ct : 0);
+    if constexpr (IN::kWin) {
+      const bool oc = valid & x.oow(ct, 4);
+      if (ballot(oc)) yv = oc ? x.g32(ct) : yv;
+    }
     order();
     tab[hh] = (uint16_t)pi;
     order();
@@ -446,9 +551,18 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint8_t* x, uint32_t n, u
 #pragma clang loop unroll(disable)
       for (;;) {                                                  // snappy.c:163-164
         const uint32_t q = at_n + lane;
+        if constexpr (IN::kWin) x.ensure(at_n + kWave);
         // Clamped unconditional reads (q < n implies r + lane < n).
         const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
-        const bool same = (q < n) & (x[ra] == x[qa]);
+        uint32_t br = x.byte(ra), bq = x.byte(qa);
+        if constexpr (IN::kWin) {
+          const bool orq = (q < n) & (x.oow(ra, 1) || x.oow(qa, 1));
+          if (ballot(orq)) {
+            br = orq ? x.gbyte(ra) : br;
+            bq = orq ? x.gbyte(qa) : bq;
+          }
+        }
+        const bool same = (q < n) & (br == bq);
         const uint64_t diff = ballot(!same);
         if (diff) {
           at_n += (uint32_t)__builtin_ctzll(diff);
@@ -554,7 +668,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   for (uint32_t c0 = 0; c0 < len; c0 += kChunk) {
     const uint32_t clen = len - c0 < kChunk ? len - c0 : kChunk;
     const uint32_t sh = stage_in(&s_in[wv][0], src + c0, clen);
-    const uint8_t* x = &s_in[wv][sh];
+    LdsIn x{&s_in[wv][sh]};
     order();
     if (clen >= kMinBlock) {
       op = encode_chunk(x, clen, &s_tab[wv][0], o, op, e0, e1);
@@ -565,6 +679,52 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   }
   if (lane == 0) out_len[i] = op;
 }
+
+// The 64 KiB class with its chunk in a W-byte LDS ring (WinIn): 32 KiB +
+// the table is 37 KB, four waves per CU (the whole-chunk image, 70 KB,
+// fits two), so C3's 1 024 blocks of 64 KiB run as one generation.
+template <uint32_t W>
+__global__ __launch_bounds__(64) void encode_win_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[W + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t s_tab[kTableCap + 8];   // + sink
+
+  const uint32_t slot = blockIdx.x;
+  if (slot >= (count ? uni(*count) : n)) return;
+  const uint32_t i = uni(index ? index[slot] : slot);
+  const uint32_t lane = lane_id();
+  uint32_t e0, e1;
+  post_copy_offsets(lane, &e0, &e1);
+  const uint32_t len = uni(in_len[i]);
+  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
+  const OutSlot o = out_slot(out, uni64(out_off[i]), len);
+  uint32_t op = emit_header(o, uni(hdr ? hdr[i] : len));
+  for (uint32_t c0 = 0; c0 < len; c0 += kChunk) {               // snappy.c:370-381
+    const uint32_t clen = len - c0 < kChunk ? len - c0 : kChunk;
+    const gptr<const uint8_t> g = src + c0;
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+    WinIn<W> x{s_ring, g - sh, sh, clen, 0};
+    if (clen >= kMinBlock) {
+      x.ensure(W / 4);
+      op = encode_chunk(x, clen, s_tab, o, op, e0, e1);
+    } else {
+      op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
+    }
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // the chunk's emission reads, before the ring is reused
+    order();
+  }
+  if (lane == 0) out_len[i] = op;
+}
+
+#ifndef LGS_ENC_WIN
+#define LGS_ENC_WIN 1
+#endif
+// The 64 KiB class (and longer blocks, chunk by chunk).
+static hipError_t launch_encode_big(const EncodeArgs& a, hipStream_t s);
 
 template <uint32_t IN_CAP, uint32_t WAVES>
 static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
@@ -591,6 +751,13 @@ static hipError_t launch_encode_small(const EncodeArgs& a, hipStream_t s) {
 constexpr uint32_t kEncCap1 = 16896;
 constexpr uint32_t kEncCap2 = 65536;
 
+static hipError_t launch_encode_big(const EncodeArgs& a, hipStream_t s) {
+  if (!LGS_ENC_WIN) return launch_encode_cls<kEncCap2, 1>(a, s);
+  hipLaunchKernelGGL((encode_win_kernel<32768>), dim3(a.n), dim3(64), 0, s, a.in, a.in_off,
+                     a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n, a.count);
+  return hipGetLastError();
+}
+
 // max_in: largest item length in the launch (<= 65536).
 // Blocks longer than 64 KiB are encoded chunk by chunk by their wave.
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
@@ -598,7 +765,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (max_in <= kEncCap0) return launch_encode_small(a, s);
   if (a.index || a.n < kSplitMinBlocks || !options().split) {
     if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
-    return launch_encode_cls<kEncCap2, 1>(a, s);
+    return launch_encode_big(a, s);
   }
   // A mixed-size batch: each size class in its own kernel (see
   // launch_decode_split), so small blocks keep their small LDS images.
@@ -618,7 +785,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   c.index = list + a.n; c.count = cnt + 1;
   if ((e = launch_encode_cls<kEncCap1, 1>(c, s)) != hipSuccess) return e;
   c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
-  if (max_in > kEncCap1 && (e = launch_encode_cls<kEncCap2, 1>(c, s)) != hipSuccess) return e;
+  if (max_in > kEncCap1 && (e = launch_encode_big(c, s)) != hipSuccess) return e;
   return scratch.release();
 }
 

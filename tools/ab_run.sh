@@ -9,9 +9,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p n
     --timeout 120 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1
 rc=$?; tail -n 3 gpurun_out/ab_pytest.log; [ $rc -eq 0 ] || exit $rc
 export PROBE_CHECK=1
-for lib in probes/base.so probes/new.so probes/base.so probes/new.so; do
-  LGS_DECODE_KERNEL=wave timeout -k 10 200 python tools/probe_ab.py $lib || exit $?
-done
+timeout -k 10 300 python tools/probe_ab.py probes/base.so probes/new.so probes/base.so probes/new.so || exit $?
 for lib in probes/base.so probes/new.so; do
   timeout -k 10 300 python tools/bench_mixed.py --lib $lib --iters 10 > gpurun_out/ab_mixed_$(basename $lib .so).json || exit $?
   python -c "
