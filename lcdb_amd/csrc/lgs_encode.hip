@@ -61,8 +61,8 @@ struct OutSlot {
 // W-byte LDS ring of the chunk with the chunk in HBM behind it, so four
 // waves fit a CU instead of two.  lcdb's 2 048-entry table keeps candidates
 // from anywhere in the chunk, but on fillseq only ~40 of a 64 KiB block's
-// 26 600 probes find one more than 28 000 bytes back (tools: the age
-// simulation in DESIGN.md), so reads outside the ring take a slow path: a
+// 26 600 probes find one more than 28 000 bytes back (tools/
+// sim_candidate_age.py), so reads outside the ring take a slow path: a
 // wave-uniform test, then global loads for the lanes that need them.
 struct LdsIn {
   static constexpr bool kWin = false;
