@@ -149,6 +149,48 @@ struct WinIn {
   }
 };
 
+// A literal's bytes [from, from + len) of the chunk to slot offset `to`,
+// 16 bytes per lane and four pieces in flight (WinIn reads them from HBM:
+// a byte per lane and load would wait a memory round trip per 64 bytes).
+// The last < 16 bytes go out as exact 8/4/2/1-byte stores.
+template <class IN>
+__device__ __forceinline__ void copy_lit16(const OutSlot& o, uint32_t op, const IN& x,
+                                           uint32_t to, uint32_t from, uint32_t len) {
+  constexpr uint32_t kOff = 0x40000000u;            // dropped by the range check
+  const uint32_t lane = lane_id();
+  const uint32_t whole = len & ~15u;
+#pragma clang loop unroll(disable)
+  for (uint32_t t0 = 0; t0 < whole; t0 += 4096) {
+    u32x4 v[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t t = t0 + 1024 * k + 16 * lane;
+      v[k] = x.lit128(from + (t < whole ? t : 0u));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t t = t0 + 1024 * k + 16 * lane;
+      o.put16(op, t < whole ? to + t : kOff, v[k]);
+    }
+  }
+  const uint32_t rem = len - whole;
+  if (rem) {
+    u32x4 v = x.lit128(from + whole);
+    uint32_t at = to + whole;
+    const bool l0 = lane == 0;
+    o.put8(op, l0 && (rem & 8) ? at : kOff, v.x, v.y);
+    if (rem & 8) v = u32x4{v.z, v.w, 0, 0};
+    at += rem & 8;
+    o.put4(op, l0 && (rem & 4) ? at : kOff, v.x);
+    if (rem & 4) v.x = v.y;
+    at += rem & 4;
+    o.put2(op, l0 && (rem & 2) ? at : kOff, v.x);
+    if (rem & 2) v.x >>= 16;
+    at += rem & 2;
+    o.put(op, l0 && (rem & 1) ? at : kOff, v.x);
+  }
+}
+
 // snappy.c:53-73: literal of len >= 1 taken from lds[from ..], written at o:
 // header (1-3 bytes) and bytes in one pass, lane j writing output byte j.
 // Returns bytes written.
@@ -161,6 +203,11 @@ __device__ __forceinline__ uint32_t emit_literal(const OutSlot& o, uint32_t op, 
   const uint32_t h0 = m < 60 ? (m << 2) : (m < 256 ? 0xf0u : 0xf4u);
   const uint32_t hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);   // little-endian header
   const uint32_t total = hl + len;
+  if constexpr (IN::kWin) {
+    if (lane < hl) o.put(op, lane, hdr >> (8 * lane));
+    copy_lit16(o, op, in, hl, from, len);
+    return total;
+  }
 #pragma clang loop unroll(disable) vectorize(disable)
   for (uint32_t j0 = 0; j0 < total; j0 += kWave) {
     const uint32_t j = j0 + lane;
@@ -319,6 +366,10 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
   for (uint64_t big = ballot(LL > kLongLit); big; big &= big - 1) {
     const uint32_t l = (uint32_t)__builtin_ctzll(big);
     const uint32_t from = lane_val(lit, l), len = lane_val(LL, l), to = lane_val(lat, l);
+    if constexpr (IN::kWin) {
+      copy_lit16(o, op, x, to, from, len);
+      continue;
+    }
 #pragma clang loop unroll(disable)
     for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
       const uint32_t j = j0 + lane;
