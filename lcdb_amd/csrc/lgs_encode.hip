@@ -203,7 +203,7 @@ __device__ __forceinline__ uint32_t emit_literal(const OutSlot& o, uint32_t op, 
   const uint32_t h0 = m < 60 ? (m << 2) : (m < 256 ? 0xf0u : 0xf4u);
   const uint32_t hdr = h0 | ((m & 0xffu) << 8) | ((m >> 8) << 16);   // little-endian header
   const uint32_t total = hl + len;
-  if constexpr (IN::kWin) {
+  if (IN::kWin || len > kWave) {
     if (lane < hl) o.put(op, lane, hdr >> (8 * lane));
     copy_lit16(o, op, in, hl, from, len);
     return total;
@@ -366,10 +366,8 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
   for (uint64_t big = ballot(LL > kLongLit); big; big &= big - 1) {
     const uint32_t l = (uint32_t)__builtin_ctzll(big);
     const uint32_t from = lane_val(lit, l), len = lane_val(LL, l), to = lane_val(lat, l);
-    if constexpr (IN::kWin) {
-      copy_lit16(o, op, x, to, from, len);
-      continue;
-    }
+    copy_lit16(o, op, x, to, from, len);
+    continue;
 #pragma clang loop unroll(disable)
     for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
       const uint32_t j = j0 + lane;
