@@ -606,7 +606,7 @@ __global__ __launch_bounds__(64) void decode_wide_kernel(
     // this window's literals), flush once 8 KiB are pending, and parse.
     w = apos;
     wend = aend - w < kWave ? aend : w + kWave;
-    while (staged < aend && staged - w <= kRefill) land();
+    while (staged < aend && staged <= w + kRefill) land();   // (staged may trail w after a long literal)
     if (made - F >= kFlushAt) {
       sb[pend] = (uint8_t)pv;                 // the last op's bytes, before they are flushed
       pend = pad;
@@ -689,12 +689,45 @@ __global__ __launch_bounds__(64) void decode_wide_kernel(
           sb[pend] = (uint8_t)pv;
           pend = pad;
           order();
-          for (uint32_t j = 0; j < nb; j += kWave) {
-            while (staged < aend && staged < x + j + kWave) land();
+          // Bytes up to the output ring's next 16-byte edge one a lane,
+          // then whole granules straight from HBM (16 bytes a lane, 4 KiB in
+          // flight: the input ring is bypassed and restaged after), then the
+          // last < 16 bytes one a lane.  Reads stay within the block's
+          // 16-byte read slack.
+          const uint32_t u0 = made + oshift;
+          const uint32_t head0 = (16u - (u0 & 15u)) & 15u;
+          const uint32_t head = head0 < nb ? head0 : nb;
+          const uint32_t body = (nb - head) & ~15u;
+          const gptr<const uint8_t> ls = src + x;
+          if (lane < head) sb[(u0 + lane) & (kOut - 1)] = ls[lane];
+          order();
+          for (uint32_t j = head; j < head + body; j += 4096) {
             if (made + j - F >= kFlushAt) flush(((made + j + oshift) & ~15u) - oshift);
-            if (j + lane < nb)
-              sb[(made + j + lane + oshift) & (kOut - 1)] = ib[(x + j + lane) & (kIn - 1)];
+            u32x4 v[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+              const uint32_t jj = j + 16 * (lane + 64 * k);
+              if (jj < head + body) v[k] = ld16(ls + jj);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+              const uint32_t jj = j + 16 * (lane + 64 * k);
+              if (jj < head + body)
+                *reinterpret_cast<u32x4*>(sb + ((u0 + jj) & (kOut - 1))) = v[k];
+            }
             order();
+          }
+          if (made + nb - F >= kFlushAt) flush(((made + head + body + oshift) & ~15u) - oshift);
+          {
+            const uint32_t jj = head + body + lane;
+            if (jj < nb) sb[(u0 + jj) & (kOut - 1)] = ls[jj];
+          }
+          order();
+          // The stream resumes at x + nb: restage from there.
+          if (x + nb > staged) {
+            __builtin_amdgcn_s_waitcnt(0x0f70);                   // the old prefetch
+            staged = (x + nb) & ~15u;
+            prefetch();
           }
           from = (made + oshift + lane) & (kOut - 1);
         } else if (ds > kFar) {
