@@ -287,7 +287,15 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
           } else {
             o[pend] = (uint8_t)pv;                               // before the piece writes
             order();
-            for (uint32_t j = lane; j < n; j += kWave) o[made + j] = base[x + j];
+            // 16 bytes a lane (unaligned ds_read/write_b128), then the last
+            // < 16 bytes one a lane.  In place, a piece's writes end 64+
+            // bytes below the next piece's reads (the in-place bound).
+            typedef u32x4 u32x4_b __attribute__((aligned(1)));
+            const uint32_t n16 = n & ~15u;
+            for (uint32_t j = 16 * lane; j < n16; j += 16 * kWave)
+              *(u32x4_b*)(o + made + j) = *(const u32x4_b*)(base + x + j);
+            order();
+            for (uint32_t j = n16 + lane; j < n; j += kWave) o[made + j] = base[x + j];
             pend = pad;                                          // the write below: harmless
             from = made + lane;
           }
