@@ -84,3 +84,16 @@ def test_corpus_digest_c3_mixed(orc, digests):
     for o, k in zip(ooff, olen):
         h.update(memoryview(out[int(o):int(o) + int(k)]))
     assert h.hexdigest() == d["comp_sha256"]
+
+
+@pytest.mark.slow
+def test_corpus_digest_c3_mixed_x32(orc, digests):
+    # The C3 mix at the scale bench.py times (43 008 blocks, 403 MB): the
+    # restatement reproduces the reference's per-block digests, which bench.py
+    # diffs the GPU's compressed blocks against.
+    d = digests["C3_mixed_x32"]
+    c = corpus.mixed(32)
+    assert c.n == d["blocks"] and c.raw_bytes == d["raw_bytes"]
+    out, ooff, olen = orc.encode_batch(c.buf, c.off, c.len, threads=8)
+    assert int(olen.sum(dtype=np.uint64)) == d["comp_bytes"]
+    assert corpus.digest_of_digests(corpus.block_digests(out, ooff, olen)) == d["comp_dd"]
