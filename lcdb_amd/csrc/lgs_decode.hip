@@ -835,8 +835,9 @@ __device__ __forceinline__ void lwr16(uint8_t* p, u32x4 v) { *(u32x4_l1*)p = v; 
 __device__ __forceinline__ void out_put(uint8_t* ob, uint32_t p, u32x4 v) {
   const uint32_t r = p & (ring::kOutRing - 1);
   lwr16(ob + r, v);
-  const int32_t r2 = r < 64 ? (int32_t)r + 256 : (r > 240 ? (int32_t)r - 256 : -16);
-  if (r < 64 || r > 240) lwr16(ob + r2, v);
+  // r < 64 or r > 240 as one unsigned compare; the second copy's offset as
+  // one select (its value for the other lanes is never used).
+  if (r - 64 > 176u) lwr16(ob + (int32_t)r + (r < 64 ? 256 : -256), v);
 }
 
 // A cooperative job (a refill or a flush) of one lane, 16 bytes: the lane
