@@ -397,32 +397,29 @@ __device__ __forceinline__ Tag parse_tag(u32x4 tv, uint32_t pos, uint32_t slen, 
   // parse literals and copies together, so branches would run both sides
   // anyway and add the exec-mask bookkeeping.
   Tag t;
-  const uint32_t tag = tv.x & 0xffu;
-  const uint32_t kind = tag & 3u;
+  const uint32_t tag = tv.x & 0xffu, kind = tag & 3u, m0 = tag >> 2;
   const uint32_t left = slen - pos;
   const uint32_t b1 = (tv.x >> 8) | (tv.y << 24);              // bytes 1..4
-  // literal, snappy.c:210-273
-  const uint32_t m0 = tag >> 2;
-  const bool ext = m0 >= 60;
-  const uint32_t extra = ext ? m0 - 59 : 0u;                    // 1..4 length bytes
+  const bool lit = kind == 0;
+  // literal, snappy.c:210-256: m0 < 60, or m0 - 59 length bytes
+  const uint32_t extra = m0 >= 60 ? m0 - 59 : 0u;
   const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
-  const uint32_t m = ext ? (b1 & emask) : m0;
-  const uint32_t lhl = 1 + extra, llen = m + 1;
-  const bool lbad = (ext && left - 1 < extra) || m >= 0x7fffffffu || llen > want - made ||
-                    llen > left - lhl;
-  // copies, snappy.c:276-324
-  const uint32_t clen = kind == 1 ? 4 + ((tag >> 2) & 7u) : 1 + (tag >> 2);
+  const uint32_t m = extra ? (b1 & emask) : m0;
+  // copies, snappy.c:276-317
+  const uint32_t clen = kind == 1 ? 4 + (m0 & 7u) : m0 + 1;
   const uint32_t cdist = kind == 1 ? ((tag & 0xe0u) << 3) | (b1 & 0xffu)
                                    : (kind == 2 ? b1 & 0xffffu : b1);
-  const uint32_t chl = kind == 1 ? 2u : (kind == 2 ? 3u : 5u);
-  const bool cbad = left < chl || cdist == 0 || cdist >= 0x80000000u || made < cdist ||
-                    clen > want - made;
-  const bool lit = kind == 0;
   t.kind = kind;
-  t.len = lit ? llen : clen;
-  t.hl = lit ? lhl : chl;
+  t.len = lit ? m + 1 : clen;
+  t.hl = lit ? 1 + extra : (kind == 3 ? 5u : kind + 1);
   t.dist = lit ? 0u : cdist;
-  t.bad = lit ? lbad : cbad;
+  // The rejects, folded: the tag's header must fit the stream (:240-256,
+  // :276-317); len > want - made is :263 / :323's length bound; a literal
+  // also needs m < 2^31 - 1 (:258) and its bytes in the stream (:263); a
+  // copy needs 0 < dist <= made (:320, :323): dist - 1 >= made as unsigned
+  // covers dist == 0 and dist >= 2^31 too, since made < 2^31.
+  t.bad = (t.hl > left) | (t.len > want - made) |
+          (lit ? (m >= 0x7fffffffu) | (t.hl + t.len > left) : (cdist - 1 >= made));
   t.next = pos + t.hl + (lit ? t.len : 0u);
   return t;
 }
