@@ -915,14 +915,14 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   // One piece (<= 64 bytes) of the current op (snappy.c:210-331) for every
   // lane whose bytes are in LDS (literal from the window, copy from the ring).
   auto piece = [&]() {
-    if (st == 1 && orem > 0 && !ofar) {
+    if ((st == 1) & (orem > 0) & !ofar) {
       const bool lit = okind == 0;
       const uint32_t piece = orem < 64 ? orem : 64;
-      if (!lit || in_have >= olp + piece) {
+      if (!lit | (in_have >= olp + piece)) {
         const uint32_t dist = odist;
-        const bool overlap = !lit && dist < piece;
-        const bool pat = overlap && dist <= 8 && (dist & (dist - 1)) == 0;
-        if (overlap && !pat) {
+        const bool overlap = !lit & (dist < piece);
+        const bool pat = overlap & (dist <= 8) & ((dist & (dist - 1)) == 0);
+        if (overlap & !pat) {
           // Period not dividing 16: chunk by chunk, each reading bytes the
           // previous ones wrote (LDS program order); chunk 0 of a period
           // < 16 is built byte by byte, later chunks copy from qq back
@@ -980,14 +980,14 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   // Parse the next tag (its bytes are in the window); a far copy's bytes are
   // loaded from the flushed output for the next trip.
   auto parse = [&](bool second) {
-    if (st == 1 && orem == 0 && pos < slen) {
+    if ((st == 1) & (orem == 0) & (pos < slen)) {
       const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
       if (in_have >= need_to) {
         const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
-        const bool far = t.kind != 0 && t.dist > kNear;
+        const bool far = (t.kind != 0) & (t.dist > kNear);
         if (t.bad) {
           st = 0;
-        } else if (!second || !far || made - F + t.len <= t.dist) {
+        } else if (!second | !far | (made - F + t.len <= t.dist)) {
           // (A far copy parsed in the second slot must find its source
           // flushed already; otherwise it waits for the next trip's first.)
           orem = t.len;
@@ -1010,7 +1010,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   };
 
   for (;;) {
-    const bool active = st == 1 && !(orem == 0 && pos >= slen && F >= made);
+    const bool active = (st == 1) & !((orem == 0) & (pos >= slen) & (F >= made));
     if (ballot(active) == 0) break;
 
     // ---- one piece of the current op for every lane whose bytes are in LDS;
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     // ---- everything issued last trip has landed: far-copy pieces (never
     // overlapping, <= 64 bytes), then the input refills.
     __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
-    if (st == 1 && orem > 0 && ofar) {
+    if ((st == 1) & (orem > 0) & ofar) {
       out_put(ob, made, fa0);
       if (orem > 16) out_put(ob, made + 16, fa1);
       if (orem > 32) out_put(ob, made + 32, fa2);
@@ -1041,8 +1041,8 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
 
     // ---- flush finished bytes; the block's last ones once the stream is
     // consumed (snappy.c:337: it must end exactly at want).
-    if (st == 1 && orem == 0 && pos >= slen && made != want) st = 0;
-    const bool fin = st == 1 && orem == 0 && pos >= slen;
+    if ((st == 1) & (orem == 0) & (pos >= slen) & (made != want)) st = 0;
+    const bool fin = (st == 1) & (orem == 0) & (pos >= slen);
     // Flush whole 128-byte lines of the destination: up to the last line
     // boundary at or below dst + made, so every interior line is written by
     // one job, once (a block's first and last lines are shared with its
@@ -1055,7 +1055,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     const uint32_t lim = lb > dpa ? (uint32_t)(lb - dpa) : 0u;
     const uint32_t fcnt = lim > F ? lim - F : (fin ? made - F : 0u);
     {
-      const bool need = st == 1 && fcnt > 0;
+      const bool need = (st == 1) & (fcnt > 0);
       const uint64_t m = ballot(need);
       const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -1098,12 +1098,12 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     // overwrite in the ring are consumed.  4 lanes per request, <= 32 a trip.
     {
       const uint32_t cons = (orem > 0 && okind == 0) ? olp : pos;
-      const bool need = st == 1 && in_req < slen && in_req <= cons + 64;
+      const bool need = (st == 1) & (in_req < slen) & (in_req <= cons + 64);
       const uint64_t m = ballot(need);
       const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
       const uint32_t total = uni((uint32_t)__builtin_popcountll(m));
-      if (need && j < 32) {
+      if (need & (j < 32)) {
         const uint64_t sp = reinterpret_cast<uint64_t>(src);
         s_job[j] = RingJob(lane, in_req, slen, sp);
       }
@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
         rm1 = r < 64 ? ra1 + kInRing : sink;
       }
       order();
-      if (need && j < 32) in_req += 64;
+      if (need & (j < 32)) in_req += 64;
     }
   }
 
