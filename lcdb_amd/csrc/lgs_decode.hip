@@ -995,7 +995,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           odist = t.dist;
           olp = pos + t.hl;
           pos = t.next;
-          ofar = okind != 0 && odist > kNear;
+          ofar = (okind != 0) & (odist > kNear);
           if (ofar) {
             // Flushed already: it ends <= made - kNear + 64 < F.
             const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
@@ -1068,16 +1068,15 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
 #pragma clang loop unroll(disable)
       for (uint32_t base = 0; base < total; base += 8) {
         const uint32_t jj = base + (lane >> 3), w = lane & 7u;
-        if (jj < total) {
-          const RingJob jb = s_job[jj];
-          if (16 * w < jb.cnt) {
-            const u32x4 v = lrd16(s_out + jb.lane() * kOutStride + 16 +
-                                  ((jb.off + 16 * w) & (kOutRing - 1)));
-            const gptr<uint8_t> g =
-                (gptr<uint8_t>)jb.ptr() + jb.off + 16 * w;
-            if (16 * w + 16 <= jb.cnt) st16(g, v);
-            else st_exact(g, v, jb.cnt - 16 * w);
-          }
+        // jj < base + 8 <= kJobs: the record is in range (stale past total).
+        const RingJob jb = s_job[jj];
+        if ((jj < total) & (16 * w < jb.cnt)) {
+          const u32x4 v = lrd16(s_out + (jb.lane() & (BL - 1)) * kOutStride + 16 +
+                                ((jb.off + 16 * w) & (kOutRing - 1)));
+          const gptr<uint8_t> g =
+              (gptr<uint8_t>)jb.ptr() + jb.off + 16 * w;
+          if (16 * w + 16 <= jb.cnt) st16(g, v);
+          else st_exact(g, v, jb.cnt - 16 * w);
         }
       }
       order();
@@ -1097,7 +1096,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     // ---- refill requests: the next 64 input bytes, once the 64 they
     // overwrite in the ring are consumed.  4 lanes per request, <= 32 a trip.
     {
-      const uint32_t cons = (orem > 0 && okind == 0) ? olp : pos;
+      const uint32_t cons = ((orem > 0) & (okind == 0)) ? olp : pos;
       const bool need = (st == 1) & (in_req < slen) & (in_req <= cons + 64);
       const uint64_t m = ballot(need);
       const uint32_t j = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
