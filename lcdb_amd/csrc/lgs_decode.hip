@@ -980,32 +980,30 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   // Parse the next tag (its bytes are in the window); a far copy's bytes are
   // loaded from the flushed output for the next trip.
   auto parse = [&](bool second) {
-    if ((st == 1) & (orem == 0) & (pos < slen)) {
-      const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
-      if (in_have >= need_to) {
-        const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
-        const bool far = (t.kind != 0) & (t.dist > kNear);
-        if (t.bad) {
-          st = 0;
-        } else if (!second | !far | (made - F + t.len <= t.dist)) {
-          // (A far copy parsed in the second slot must find its source
-          // flushed already; otherwise it waits for the next trip's first.)
-          orem = t.len;
-          okind = t.kind == 0 ? 0u : 1u;
-          odist = t.dist;
-          olp = pos + t.hl;
-          pos = t.next;
-          ofar = (okind != 0) & (odist > kNear);
-          if (ofar) {
-            // Flushed already: it ends <= made - kNear + 64 < F.
-            const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
-            fa0 = ld16(sp);
-            if (orem > 16) fa1 = ld16(sp + 16);
-            if (orem > 32) fa2 = ld16(sp + 32);
-            if (orem > 48) fa3 = ld16(sp + 48);
-          }
-        }
-      }
+    // Computed on every lane and committed with selects: one exec-mask
+    // region (the far-copy loads) instead of three nested ones.  Lanes that
+    // are not parsing read their own ring (in range) and discard the tag.
+    const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
+    const bool ready = (st == 1) & (orem == 0) & (pos < slen) & (in_have >= need_to);
+    const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
+    const bool far = (t.kind != 0) & (t.dist > kNear);
+    if (ready & t.bad) st = 0;
+    // (A far copy parsed in the second slot must find its source flushed
+    // already; otherwise it waits for the next trip's first.)
+    const bool take = ready & !t.bad & (!second | !far | (made - F + t.len <= t.dist));
+    orem = take ? t.len : orem;
+    okind = take ? (t.kind == 0 ? 0u : 1u) : okind;
+    odist = take ? t.dist : odist;
+    olp = take ? pos + t.hl : olp;
+    pos = take ? t.next : pos;
+    ofar = take ? far : ofar;
+    if (take & far) {
+      // Flushed already: it ends <= made - kNear + 64 < F.
+      const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
+      fa0 = ld16(sp);
+      if (orem > 16) fa1 = ld16(sp + 16);
+      if (orem > 32) fa2 = ld16(sp + 32);
+      if (orem > 48) fa3 = ld16(sp + 48);
     }
   };
 
