@@ -409,36 +409,51 @@ constexpr bool probe_off_matches_table() {
 }
 static_assert(probe_off_matches_table(), "closed-form probe schedule != snappy.c:138-143");
 
-// Index of the scratch slot every table / lane-id array carries past its
-// 2048 real entries: lanes that must not touch a real entry write there
-// instead of branching around the store (keeps the batch free of exec-mask
-// regions, whose save/branch/restore is scalar work).
+// Index of the scratch slot every table carries past its 2048 real entries:
+// lanes that must not touch a real entry aim their table access there
+// instead of branching around it (keeps the batch free of exec-mask regions,
+// whose save/branch/restore is scalar work).
 constexpr uint32_t kSink = kTableCap;
+
+// LDS address (32-bit, address space 3) of a __shared__ pointer.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+
+// tab[h] = v, returning the entry's previous value, as one LDS atomic on the
+// dword holding the u16 entry (ds_mskor_rtn_b32: mem = (mem & ~mask) | data).
+// The lanes of one such instruction that hit the same dword are applied in
+// ascending lane order, each seeing its predecessors' writes (measured on
+// gfx950, tools/lds_atomic_probe.hip; encode_chunk verifies it per batch).
+__device__ __forceinline__ uint32_t tab_swap(uint16_t* tab, uint32_t h, uint32_t v) {
+  const uint32_t sh = (h & 1u) * 16u;
+  uint32_t old;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old)
+               : "v"(lds_addr(tab) + (h >> 1) * 4u), "v"(0xffffu << sh), "v"(v << sh)
+               : "memory");
+  return (old >> sh) & 0xffffu;
+}
 
 // Encode one chunk x[0..n), 17 <= n <= 65536, held in LDS.  `tab` is the
 // u16 hash table (with a sink slot).  Writes to o, returns bytes written.
 // Mirrors snappy.c:104-195 step for step.
 //
-// Literal-search batches.  Probe index pi = 63 - lane (lane 63 takes the
-// earliest probe).  Each lane first reads its candidate from the table;
-// then each valid probe scatters pi into tab[hash] itself (the table
-// doubles as the lane-id scratch: no second 2048-entry array, so more waves
-// fit in LDS) and every lane writes its candidate back before the commit
-// write.  The LDS
-// keeps one writer per address (on gfx950 the highest lane, i.e. the
-// earliest probe -- but nothing below depends on which).  A probe that reads
-// back another pi ("loser") shares its hash with another probe of the
-// batch.  Losers then scatter their pi again (winners do not), which
-// singles out the second member of each hash group.  When every loser sees its group's
-// winners before itself (checked with a ballot), the winner is the
-// earliest probe of the group and:
-//   * a group's first probe takes its candidate from the table,
-//   * its second probe takes the first probe's position (the serial loop
-//     would have just written it), and
-//   * the batch is cut before the first third member of any group.
-// Otherwise the batch is cut before the earliest loser (lanes before it
-// share no hash with an earlier lane; the first lane never does).  Among the
-// committed probes each group's latest member writes the table.
+// Literal-search batches.  Lane l takes the batch's probe l (lane 0 the
+// earliest).  Each valid lane swaps its probe position into tab[hash] with
+// one LDS atomic (tab_swap).  Because a wave's atomics on one address apply
+// in lane order, every lane gets back exactly what snappy.c:146-148 would
+// read at that probe -- the position of the batch's latest earlier probe
+// with the same hash, else the entry as the batch found it -- and the table
+// ends as the serial loop would leave it after all 64 probes.  No lane-id
+// rounds and no cut: any number of probes may share a hash.  The first lane
+// whose 4-byte compare matches ends the search; the probes after it must not
+// have written, so in each slot they touched the first of them restores the
+// value it received (its received value is a committed position or an old
+// entry exactly when it is at most the match's position: positions grow
+// with the lane, old entries lie before the batch).  A lane receiving a
+// position later than its own would mean the order assumption broke; then
+// the batch restores the table and replays the swaps one lane at a time.
 //
 // A found match is extended; lcdb's immediate re-probe (snappy.c:172-186)
 // is folded into the next batch (below).  The literal + copy is not emitted
@@ -449,7 +464,6 @@ template <class IN>
 __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* tab,
                                  const OutSlot& o, uint32_t op0, uint32_t e0, uint32_t e1) {
   const uint32_t lane = lane_id();
-  const uint32_t pi = 63 - lane;                      // probe index in the batch
   const uint32_t last = n - kMargin;                  // snappy.c:106
 
   uint32_t tsize = 256, shift = 24;                   // snappy.c:108-125
@@ -467,7 +481,7 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   uint32_t lit = 0;      // first byte not yet emitted (snappy.c:111 "emit")
   uint32_t at = 0;       // end of the last copy
   uint32_t start = 1;    // first probe position of the current search (snappy.c:112)
-  uint32_t kv = 2;       // virtual probe index of this batch's first lane
+  uint32_t kv = 2;       // virtual probe index of this batch's lane 0
   // Recorded ops (lane k = op k), their count, op 0's literal start.
   uint32_t recA = 0, recB = 0, nops = 0, lit0 = 0;
 
@@ -476,8 +490,8 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   //   v = 1: B, position at   -- its insert and 64-bit compare (snappy.c:177-182),
   //   v >= 2: search probe v-2 from start = at+1 (snappy.c:133-154).
   // A and B exist only after a copy (a chunk's first search starts at
-  // v = 2).  They are ordinary probes to the collision logic, which gives
-  // the serial order's table semantics (B's candidate is at-1 when A and B
+  // v = 2).  They are ordinary probes to the table swap, which gives the
+  // serial order's table semantics (B's candidate is at-1 when A and B
   // share a hash); A never matches, and B's match is the re-match of
   // snappy.c:182.  Folding the re-probe into the batch removes its three
   // dependent LDS round trips from every copy.
@@ -487,11 +501,11 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   // variable and compare chains from the compiler's loop-exit unification:
   // scalar work on every trip.)
   for (;;) {
-    const uint32_t v = kv + pi;
+    const uint32_t v = kv + lane;
     uint32_t o0 = e0, o1 = e1;                      // kv == 0: see encode_kernel
     bool in_tab = true;
     if (kv != 0) {                                  // other batches: later schedule
-      const uint32_t kk = v - 2;                    // (wraps for v < 2: unused)
+      const uint32_t kk = v - 2;                    // (kv >= 2 here)
       if (kv + 62 <= kProbeClosed) {                // a chunk's first batch: no load
         o0 = probe_off(kk);
         o1 = probe_off(kk + 1);
@@ -512,7 +526,7 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     const uint64_t vmask = ballot(valid);
     const uint32_t p = valid ? start + o0 : 0;
 
-    if constexpr (IN::kWin) x.ensure(start + lane_val(o0, 0) + 16);   // lane 0: the last probe
+    if constexpr (IN::kWin) x.ensure(start + lane_val(o0, 63) + 16);  // lane 63: the last probe
     uint64_t xw = x.rd64(p);                                      // bytes p .. p+7
     if constexpr (IN::kWin) {
       const bool op_ = valid & x.oow(p, 8);
@@ -520,47 +534,25 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     }
     const uint32_t xv = (uint32_t)xw;
     const uint32_t hh = valid ? hash32(xv, shift) : kSink;
-    // The table read and the candidate's bytes do not depend on the
-    // lane-id rounds below: issue them first so their LDS latency overlaps.
-    const uint32_t ct = tab[hh];                                  // snappy.c:146, :177
-    uint32_t yv = x.rd32(valid ? ct : 0);
-    if constexpr (IN::kWin) {
-      const bool oc = valid & x.oow(ct, 4);
-      if (ballot(oc)) yv = oc ? x.g32(ct) : yv;
-    }
-    order();
-    tab[hh] = (uint16_t)pi;
-    order();
-    const uint32_t w1 = tab[hh];
-    const bool loser = valid & (w1 != pi);
-    const uint64_t lmask = ballot(loser);
-    uint32_t ncut = 64, w2 = 0xffu;
-    uint64_t second = 0;                                          // lanes comparing to their group's first
-    if (lmask) {
-      // Round two: only losers write, so a group without a loser still
-      // reads its winner back (w2 == w1).
-      tab[loser ? hh : kSink] = (uint16_t)pi;
+    // snappy.c:146-148 (and :175, :179 for A and B) for all 64 probes at once.
+    uint32_t prev = tab_swap(tab, hh, p);
+    if (ballot(valid & (prev > p))) {
+      // Not in lane order (never seen on gfx950): put back each touched
+      // slot's entry as the batch found it (the one lane per slot that
+      // received a value from before the batch), then swap lane by lane.
+      const uint32_t p0 = lane_val(p, 0);
+      tab[(valid & (prev < p0)) ? hh : kSink] = (uint16_t)prev;
       order();
-      const uint32_t r2 = tab[hh];
-      w2 = r2 == w1 ? 0xffu : r2;                                // winners: 2nd member or none
-      const uint32_t wmax = w1 > r2 ? w1 : r2;
-      if (ballot(loser & (wmax > pi))) {                          // a group out of order
-        const uint32_t first = (uint32_t)__builtin_clzll(lmask);  // earliest loser
-        ncut = first > 1 ? first : 1;
-        // Past the cut nothing commits, except probe 0 (lane 63) when it is a
-        // loser: its group's winner leaves it the slot (w2 = 0), all other
-        // winners own theirs (w2 past every commit).
-        const bool with0 = ((lmask >> 63) & 1) && hh == lane_val(hh, 63);
-        w2 = with0 ? 0u : 0xffu;
-      } else {
-        const uint64_t third = ballot(loser & (w2 != pi));
-        ncut = third ? (uint32_t)__builtin_clzll(third) : 64u;
-        second = lmask;
-        // A group's second probe compares against the first probe's
-        // bytes, which that lane already holds.
-        const uint32_t xfirst = __shfl(xv, 63 - (w1 & 63));
-        yv = loser ? xfirst : yv;
+      for (uint64_t r = vmask; r; r &= r - 1) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(r);
+        const uint32_t got = tab_swap(tab, lane == l ? hh : kSink, p);
+        prev = lane == l ? got : prev;
       }
+    }
+    uint32_t yv = x.rd32(valid ? prev : 0);
+    if constexpr (IN::kWin) {
+      const bool oc = valid & x.oow(prev, 4);
+      if (ballot(oc)) yv = oc ? x.g32(prev) : yv;
     }
     // snappy.c:152; A never matches; B is lcdb's 64-bit compare (snappy.c:182):
     // bytes at..at+6 against a zero-extended 4-byte load.
@@ -569,31 +561,20 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     // (Bitwise, not ?: -- as a select chain on v the compiler lowers it
     // to a divergent switch.)
     const bool mt = eq & !isA & (!isB | hi0);
-    const uint64_t mm = ballot((pi < ncut) & mt) & vmask;
-    const uint32_t ncommit = mm ? (uint32_t)__builtin_clzll(mm) + 1 : ncut;
-    // snappy.c:148, :175, :179, and undoing the lane-id scatters, in one
-    // store per lane: every slot the batch touched gets its final value from
-    // exactly one lane.  A group's second probe (a loser) writes its position
-    // if it commits; the group's first probe (or a probe alone in its slot)
-    // writes its position if it commits, else the slot's old entry ct --
-    // unless its second commits (w2 < ncommit), which then owns the slot.
-    // Everything else (probes past the cut, invalid lanes) hits the sink.
-    // (Two stores, undo-all then commit, cost one more random LDS access per
-    // batch: about 3 % of the encode time.)
-    const bool commit = pi < ncommit;
-    const bool owner = loser ? commit : !(w2 < ncommit);
-    tab[owner ? hh : kSink] = (uint16_t)(commit ? p : ct);
-    order();
+    const uint64_t mm = ballot(mt) & vmask;
 
     // The match path computes the copy's end; both paths then update the
     // loop state with selects (one set of loop-carried values, no per-path
     // copies of them at the latch).
     uint32_t at_n = at;
     if (mm) {
-      const uint32_t src = 63 - (ncommit - 1);
-      const uint32_t base = lane_val(p, src);
-      const uint32_t ref = ((second >> src) & 1) ? lane_val(p, 63 - (lane_val(w1, src) & 63))
-                                                 : lane_val(ct, src);
+      const uint32_t m = (uint32_t)__builtin_ctzll(mm);           // the matching probe
+      const uint32_t base = lane_val(p, m);
+      const uint32_t ref = lane_val(prev, m);
+      // The probes after it did not happen: in each slot they touched, the
+      // first of them puts back what it received.
+      tab[(valid & (lane > m) & (prev <= base)) ? hh : kSink] = (uint16_t)prev;
+      order();
       // ---- the copy (snappy.c:158-169)
       uint32_t r = ref + 4;
       at_n = base + 4;
@@ -632,12 +613,12 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
       }
     }
     // Match: the search restarts after the copy (snappy.c:169, 184-185).
-    // No match: it ends if a probe before the cut was past the limit, else
-    // continues after the cut.
-    const bool done = mm ? at_n >= last : (uint32_t)__builtin_popcountll(vmask) < ncut;
+    // No match: it ends if a probe of the batch was past the limit
+    // (snappy.c:143), else continues with the next 64 probes.
+    const bool done = mm ? at_n >= last : vmask != ~0ull;
     lit = mm ? at_n : lit;
     start = mm ? at_n + 1 : start;
-    kv = mm ? 0u : kv + ncut;
+    kv = mm ? 0u : kv + kWave;
     at = at_n;
     if (done) break;
   }
@@ -648,14 +629,14 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
 }
 
 // Offsets, relative to the batch's start = at + 1, of each lane's probe in
-// the batch right after a copy: lane 63 is the re-probe's A (at - 1), lane 62
-// its B (at), lane l < 62 search probe 61 - l; e1 is the offset of the probe
+// the batch right after a copy: lane 0 is the re-probe's A (at - 1), lane 1
+// its B (at), lane l >= 2 search probe l - 2; e1 is the offset of the probe
 // after it (the bound check of snappy.c:143; A and B always pass it, the
 // batch runs only while at < last).
 __device__ __forceinline__ void post_copy_offsets(uint32_t lane, uint32_t* e0, uint32_t* e1) {
-  const uint32_t pk = (63 - lane) >= 2 ? 61 - lane : 0;
-  *e0 = lane == 63 ? 0xfffffffeu : (lane == 62 ? 0xffffffffu : probe_off(pk));
-  *e1 = lane >= 62 ? 0u : probe_off(pk + 1);
+  const uint32_t pk = lane >= 2 ? lane - 2 : 0;
+  *e0 = lane == 0 ? 0xfffffffeu : (lane == 1 ? 0xffffffffu : probe_off(pk));
+  *e1 = lane < 2 ? 0u : probe_off(pk + 1);
 }
 
 // varint32 header hv (coding.h:140-167) at the slot's start, unless hv is
@@ -698,8 +679,8 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
-  // Probe offsets of search probes pi - 2 (the batch right after a copy,
-  // whose lanes pi = 0, 1 are the re-probe), kept in registers.  Relative
+  // Probe offsets of search probes lane - 2 (the batch right after a copy,
+  // whose lanes 0 and 1 are the re-probe), kept in registers.  Relative
   // to that batch's start = at + 1 the re-probe's positions are A = at - 1
   // (offset -2) and B = at (-1), and both are always in bounds (the batch
   // runs only while at < last): offset 0 for their bound check.
