@@ -126,7 +126,10 @@ def _free_port() -> int:
 
 def spawn_ranks(n: int, argv: list[str]) -> int:
     """Start n rank processes of this script (this process never touches a
-    GPU) and return the first non-zero exit status, else 0."""
+    GPU) and return the first non-zero exit status, else 0.  The children
+    are polled: once one fails the others are terminated at once (they
+    would otherwise sit in gloo's rendezvous or a barrier until its
+    timeout)."""
     port = _free_port()
     procs = []
     for r in range(n):
@@ -134,9 +137,18 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
                                       env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    first_bad = 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad and not first_bad:
+            first_bad = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+        if all(rc is not None for rc in rcs):
+            return first_bad
+        time.sleep(0.05)
 
 
 # ---------------------------------------------------------------- ranks
@@ -183,8 +195,13 @@ def main(argv=None) -> int:
 
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # A short timeout: a rank that died must not leave the others waiting
+        # for gloo's default 30 minutes.
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=300))
     try:
         if a.plan_only:
             run_plan_only(a, rank, world, dist)
@@ -253,6 +270,11 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
     if dist:
         dist.barrier()
     elapsed = shard.max_over_ranks(t1 - t0, dist)
+    # every rank's own elapsed time (imbalance between GPUs is visible here)
+    per_rank = [t1 - t0]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, t1 - t0)
 
     # ---- extra (not `value`): encode and decode concurrently on two streams,
     # step k encoding copy k while decoding what step k-1 encoded -- the shape
@@ -360,8 +382,8 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
             "frac_of_achievable": (kern[dom]["achieved_GBps"] / copy_gbps) if copy_gbps else None}
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(c, a, hc)
+    if rank == 0 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(c, a, hc, world)
 
     # ---- extra (not `value`): BASELINE.json configs[2] on this GPU, after
     # everything above, with its own buffers (the C2 ones are freed first).
@@ -388,6 +410,8 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
                                    "N-GPU measurement" % (world, ndev)) if shared
                                   else "one GPU per rank",
                        "copies_rotated": a.copies},
+            "per_rank_elapsed_s": {"min": min(per_rank), "max": max(per_rank),
+                                   "ranks": [round(x, 6) for x in per_rank]},
             "encode_GiBps": raw_bytes * world / (enc_ms * 1e-3) / 2**30,
             "decode_GiBps": raw_bytes * world / (dec_ms * 1e-3) / 2**30,
             "kernels": kern, "roofline": roof, "cpu_baseline": cpu, "parity": parity,
@@ -512,19 +536,28 @@ def cpu_threads_share(a) -> int:
     return max(1, min(16, share))
 
 
-def cpu_baseline(c, a, gpu_comp) -> dict:
+def cpu_baseline(c, a, gpu_comp, world: int) -> dict:
     """BASELINE.md's CPU-baseline plan: the reference snappy.c (oracle/_ref,
     compiled unmodified) over the first `--cpu-sample` of this GPU's blocks
-    (all of C2), 1 thread and the host's thread share, outputs pre-faulted,
-    warm-up + median of 5, compressed bytes checked against the GPU's."""
+    (all of C2), at 1 thread, at the host's per-GPU thread share and at
+    `nproc` threads (the process's affinity set: the whole node), warm-up +
+    median of 5, compressed bytes checked against the GPU's.  Multi-thread
+    points run with both block partitions of cpu_batch.c (static
+    round-robin, as the plan says, and contiguous), each into fresh
+    buffers first-touched by its own worker threads (NUMA-local pages);
+    the headline is the `nproc` point's faster partition -- the node's
+    CPUs against the node's GPUs (at N > 1 this is rank 0's node-level
+    comparison).  `cores` = physical cores the threads occupy."""
     import oracle
     codec, kind = oracle.reference(), "reference"
     if codec is None:
         codec, kind = oracle.restatement(), "port"
-    nt = cpu_threads_share(a)
+    share = cpu_threads_share(a)
+    nproc = len(os.sched_getaffinity(0))
     m = min(a.cpu_sample, c.n)
     off, ln = c.off[:m].copy(), c.len[:m].copy()
-    plan = oracle.baseline_plan(codec, c.buf, off, ln, sorted({1, nt}), reps=a.cpu_reps)
+    counts = sorted({1, share, nproc})
+    plan = oracle.baseline_plan(codec, c.buf, off, ln, counts, reps=a.cpu_reps, partitions=(0, 1))
     same = None
     if gpu_comp is not None:
         from lcdb_amd import corpus
@@ -533,18 +566,29 @@ def cpu_baseline(c, a, gpu_comp) -> dict:
                                    corpus.block_digests(gpu_comp.buf, gpu_comp.off[:m],
                                                         gpu_comp.len[:m])))
     pt = plan["per_threads"]
+    pname = {0: "round-robin", 1: "contiguous"}
+
+    def point(t: int) -> dict:
+        parts = {pname[p]: {k: v[k] for k in ("roundtrip_GiBps", "encode_GiBps", "decode_GiBps")}
+                 for (tt, p), v in pt.items() if tt == t}
+        best = max(parts, key=lambda k: parts[k]["roundtrip_GiBps"])
+        return dict(parts[best], threads=t, cores=oracle.cores_for_threads(t), partition=best,
+                    by_partition=parts)
+
+    top = point(nproc)
     host = oracle.cpu_model()
-    return {"value": pt[nt]["roundtrip_GiBps"], "unit": "GiB/s", "cores": nt,
-            "threads": nt, "kind": kind,
-            "encode_GiBps": pt[nt]["encode_GiBps"], "decode_GiBps": pt[nt]["decode_GiBps"],
-            "single_thread": {k: pt[1][k] for k in ("roundtrip_GiBps", "encode_GiBps",
-                                                     "decode_GiBps")},
+    return {"value": top["roundtrip_GiBps"], "unit": "GiB/s", "cores": top["cores"],
+            "threads": nproc, "kind": kind, "partition": top["partition"],
+            "encode_GiBps": top["encode_GiBps"], "decode_GiBps": top["decode_GiBps"],
+            "nproc": top, "per_gpu_share": point(share), "single_thread": point(1),
             "cpu_model": host["model"], "physical_cores": host["physical_cores"],
             "logical_cpus": host["logical_cpus"], "affinity_cpus": host["affinity_cpus"],
+            "affinity_physical_cores": host["affinity_physical_cores"],
+            "numa_nodes": host["numa_nodes"], "gpus_in_this_run": world,
             "same_bytes_as_gpu": same,
-            "sample": f"first {m} of the GPU's blocks ({plan['raw_bytes']} B raw), "
-                      f"encode then decode, warm-up + median of {a.cpu_reps} runs, "
-                      f"1 and {nt} threads (static round-robin), pre-faulted outputs"}
+            "sample": f"first {m} of rank 0's blocks ({plan['raw_bytes']} B raw), encode then "
+                      f"decode, warm-up + median of {a.cpu_reps} runs, at {counts} threads "
+                      f"(round-robin and contiguous partitions, NUMA-local outputs)"}
 
 
 if __name__ == "__main__":

@@ -25,6 +25,8 @@ CORPUS_LIB = os.path.join(PKG, "libcorpus.so")
 HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip",
                "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp", "lgs_probe.hip"]
 HIP_HEADERS = ["lgs_device.h", "lgs_launch.h"]
+# Only ldb_snappy_* and lgs_* are exported (the library is loaded into lcdb).
+EXPORTS_MAP = os.path.join(CSRC, "exports.map")
 # The files that define the two profiled codec kernels and how they are
 # launched (grid, LDS class, split); the host runtime, table and bloom
 # sources do not change what encode_kernel / decode_ring_kernel execute.
@@ -66,12 +68,13 @@ def _run(cmd: list[str]) -> None:
 def build_hip(force: bool = False, extra: list[str] | None = None, out: str = LIB) -> str:
     """The codec library; `out` / `extra` make probe builds (tools/probe_ab.py)."""
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [
+    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [EXPORTS_MAP,
         os.path.join(ROOT, "include", "lcdb_gpu_snappy.h")]
     if force or _stale(out, deps):
         tmp = out + ".tmp"
         _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wextra", "-pthread", *srcs, "-o", tmp, *(extra or [])])
+              "-Wall", "-Wextra", "-pthread", f"-Wl,--version-script={EXPORTS_MAP}", *srcs,
+              "-o", tmp, *(extra or [])])
         os.replace(tmp, out)
     return out
 

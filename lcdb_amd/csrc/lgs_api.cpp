@@ -29,8 +29,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -474,8 +476,13 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
   return 0;
 }
 
+// LGS_DIE_EXIT=<code>: exit with that code instead of abort() (tests drive
+// the failure paths in child processes without a SIGABRT on the GPU box).
 [[noreturn]] void die(const char* what) {
   fprintf(stderr, "lcdb_gpu_snappy: %s failed: %s\n", what, t_err);
+  fflush(stderr);
+  const char* e = getenv("LGS_DIE_EXIT");
+  if (e && atoi(e) > 0) _exit(atoi(e));
   abort();
 }
 
@@ -588,6 +595,33 @@ int host_verdict(uint32_t want, size_t m) {
   return -1;
 }
 
+// Device memory for an over-slot decode.  A valid stream must never come
+// back as corrupt because memory is short for a moment (lcdb
+// would turn that 0 into a lasting LDB_CORRUPTION background error), so a
+// failed hipMalloc is retried with a growing back-off (about 2 s in all)
+// before the call fails -- and then ldb_snappy_decode aborts with a
+// diagnostic, as on any other device failure.  Test hook:
+// lgs_set_option("inject_alloc_failures", "N") makes the next N attempts
+// fail as if the device were out of memory.
+std::atomic<int> g_inject_alloc_failures{0};
+
+int big_alloc(uint8_t** p, size_t bytes, uint32_t want) {
+  unsigned wait_us = 500;
+  for (int attempt = 0;; ++attempt) {
+    int inj = g_inject_alloc_failures.load();
+    bool injected = false;
+    while (inj > 0 && !(injected = g_inject_alloc_failures.compare_exchange_weak(inj, inj - 1))) {
+    }
+    if (!injected && hipMalloc(p, bytes) == hipSuccess) return LGS_OK;
+    if (!injected) (void)hipGetLastError();
+    if (attempt == 12)
+      return fail(LGS_ENOMEM, "hipMalloc(%zu) for a %u-byte block failed %d times", bytes, want,
+                  attempt + 1);
+    std::this_thread::sleep_for(std::chrono::microseconds(wait_us));
+    wait_us = wait_us < 256000 ? 2 * wait_us : wait_us;
+  }
+}
+
 // Decode one host block on the GPU.  *ok = reference decode result.
 int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   *ok = 0;
@@ -599,9 +633,13 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
     *ok = hv;
     return LGS_OK;
   }
-  // (Blocks are addressed with 32-bit lengths on the device; lcdb's blocks
-  // are far smaller.)
-  if (xn > 0xffffffffu) return fail(LGS_ENOMEM, "a %zu-byte stream is too large", xn);
+  // Blocks are addressed with 32-bit lengths on the device.  A stream this
+  // long passed host_verdict (want >= xn / 6 > 700 MB) and may be valid, so
+  // it is not reported as corrupt: the call fails as unsupported.  (lcdb's
+  // blocks are 4 KiB - a few MiB; format.c reads a block's bytes from the
+  // file before decoding, so only a real multi-GiB block gets here.)
+  if (xn > 0xffffffffu)
+    return fail(LGS_EINVAL, "a %zu-byte stream exceeds the device decoder's 4 GiB limit", xn);
   const uint32_t n = (uint32_t)xn;
   Lease lease(dropin_pool());
   LGS_TRY(lease.acquire());
@@ -648,8 +686,7 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   // the status says ok.
   uint8_t* big = nullptr;
   const size_t big_bytes = align_up((size_t)n + 16, 256) + align_up((size_t)want + 16, 256);
-  if (hipMalloc(&big, big_bytes) != hipSuccess)
-    return fail(LGS_ENOMEM, "hipMalloc(%zu) for a %u-byte block failed", big_bytes, want);
+  LGS_TRY(big_alloc(&big, big_bytes, want));
   struct Free {
     uint8_t* p;
     ~Free() { (void)hipFree(p); }
@@ -736,17 +773,12 @@ int ldb_snappy_decode_size(size_t* zn, const uint8_t* xp, size_t xn) {   // snap
 }
 
 int ldb_snappy_decode(uint8_t* zp, const uint8_t* xp, size_t xn) {
-  // format.c:237-251 turns 0 into LDB_CORRUPTION.  Running out of device
-  // memory for a block larger than a drop-in slot reports 0 as well (with a
-  // diagnostic): the reference cannot fail that way and lcdb has no other
-  // code for it.  Anything else is a lost device: abort loudly.
+  // format.c:237-251 turns 0 into LDB_CORRUPTION, so 0 means exactly the
+  // reference's 0.  A call that cannot run (device memory still short after
+  // big_alloc's retries, a lost device, a stream beyond the device's 4 GiB
+  // addressing) is not a corrupt block: it aborts with a diagnostic.
   int ok = 0;
-  const int rc = decode_one(zp, xp, xn, &ok);
-  if (rc == LGS_ENOMEM) {
-    fprintf(stderr, "lcdb_gpu_snappy: ldb_snappy_decode: %s\n", t_err);
-    return 0;
-  }
-  if (rc != LGS_OK) die("ldb_snappy_decode");
+  if (decode_one(zp, xp, xn, &ok) != LGS_OK) die("ldb_snappy_decode");
   return ok;
 }
 
@@ -769,6 +801,14 @@ int lgs_set_option(const char* name, const char* value) {
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
     else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
+    return LGS_OK;
+  }
+  if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)
+    char* end = nullptr;
+    const long v = strtol(value, &end, 10);
+    if (!*value || *end || v < 0 || v > 1000000)
+      return fail(LGS_EINVAL, "inject_alloc_failures '%s' (0..1000000)", value);
+    g_inject_alloc_failures = (int)v;
     return LGS_OK;
   }
   if (!strcmp(name, "split")) {
@@ -1002,7 +1042,7 @@ struct ReadScratch {
   }
 };
 
-int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const uint32_t* d_raw_len,
+static int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const uint32_t* d_raw_len,
                 uint32_t n, uint32_t max_raw_len, int compression, uint64_t base, uint8_t* d_file,
                 uint64_t* d_handle_off, uint64_t* d_handle_size, uint64_t* d_end, uint8_t* scratch,
                 const WriteScratch& W, hipStream_t s) {
@@ -1025,7 +1065,7 @@ int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const uint32_t*
   return LGS_OK;
 }
 
-int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* d_hoff,
+static int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* d_hoff,
                const uint64_t* d_hsize, uint32_t n, int verify, uint8_t* d_out,
                const uint64_t* d_out_off, const uint32_t* d_out_cap, uint32_t max_out_cap,
                uint32_t* d_out_len, uint8_t* d_status, uint8_t* scratch, const ReadScratch& R,
@@ -1329,14 +1369,14 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
 
 namespace {
 
-uint32_t bloom_k(int bpk) {                        // bloom.c:35-45
+static uint32_t bloom_k(int bpk) {                        // bloom.c:35-45
   size_t k = (size_t)(bpk * 0.69);
   if (k < 1) k = 1;
   if (k > 30) k = 30;
   return (uint32_t)k;
 }
 
-size_t bloom_bytes(uint64_t n, int bpk) {          // bloom.c:69-80
+static size_t bloom_bytes(uint64_t n, int bpk) {          // bloom.c:69-80
   uint64_t bits = n * (uint64_t)bpk;
   if (bits < 64) bits = 64;
   return (size_t)((bits + 7) / 8);
@@ -1523,7 +1563,7 @@ struct FilterScratch {
   }
 };
 
-int filter_args(uint32_t nblocks, uint64_t data_end, int bits_per_key, int internal_keys) {
+static int filter_args(uint32_t nblocks, uint64_t data_end, int bits_per_key, int internal_keys) {
   if (bits_per_key < 0 || bits_per_key > kMaxBitsPerKey)
     return fail(LGS_EINVAL, "bits_per_key %d out of range", bits_per_key);
   if (data_end >= kMaxDataEnd) return fail(LGS_EINVAL, "data_end %llu too large",

@@ -67,6 +67,8 @@ struct OutSlot {
 struct LdsIn {
   static constexpr bool kWin = false;
   const uint8_t* x;
+  // (Aligned dwords + v_alignbyte: the same reads as unaligned ds_read_b64 /
+  // b32 took C2 encode from 783 to 1 515 us, profiles/r3d_unaligned_lds_ab.txt.)
   __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(x, p); }
   __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(x, p); }
   __device__ uint32_t byte(uint32_t p) const { return x[p]; }
@@ -367,13 +369,6 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
     const uint32_t l = (uint32_t)__builtin_ctzll(big);
     const uint32_t from = lane_val(lit, l), len = lane_val(LL, l), to = lane_val(lat, l);
     copy_lit16(o, op, x, to, from, len);
-    continue;
-#pragma clang loop unroll(disable)
-    for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
-      const uint32_t j = j0 + lane;
-      const uint32_t b = x.litbyte(from + (j < len ? j : 0u));
-      o.put(op, j < len ? to + j : kOff, b);
-    }
   }
   // 3. headers and tags.
   o.put(op, hl > 0 ? excl : kOff, hdr);

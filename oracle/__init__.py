@@ -71,9 +71,10 @@ class Codec:
 
     # -- batches (pthreads, static round-robin partition: cpu_batch.c) --
 
-    def _batch(self, mode: int, fn, threads, buf, off, ln, out, ooff, olen, status):
+    def _batch(self, mode: int, fn, threads, buf, off, ln, out, ooff, olen, status,
+               partition: int = 0):
         drv = _driver()
-        rc = drv.cpu_batch_run(mode, C.cast(fn, C.c_void_p), threads,
+        rc = drv.cpu_batch_run2(mode, C.cast(fn, C.c_void_p), threads, partition,
                                buf.ctypes.data, off.ctypes.data, ln.ctypes.data,
                                out.ctypes.data, ooff.ctypes.data,
                                olen.ctypes.data if olen is not None else None,
@@ -114,6 +115,9 @@ def _driver():
         d = C.CDLL(ORACLE_SO, mode=C.RTLD_LOCAL)
         d.cpu_batch_run.restype = C.c_int
         d.cpu_batch_run.argtypes = [C.c_int, C.c_void_p, C.c_int] + [C.c_void_p] * 7 + [C.c_uint32]
+        d.cpu_batch_run2.restype = C.c_int
+        d.cpu_batch_run2.argtypes = ([C.c_int, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 7
+                                     + [C.c_uint32])
         _drv = d
     return _drv
 
@@ -366,8 +370,33 @@ def time_cpu(codec: Codec, mode: str, buf, off, ln, threads: int, comp=None,
     return float(np.median(times)), reps
 
 
+def _affinity_cores(cpus) -> int | None:
+    """Physical cores (package, core id) behind a set of logical CPUs."""
+    cores = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(base + "core_id") as f:
+                core = f.read().strip()
+            with open(base + "physical_package_id") as f:
+                pkg = f.read().strip()
+        except OSError:
+            return None
+        cores.add((pkg, core))
+    return len(cores) or None
+
+
+def cores_for_threads(threads: int) -> int:
+    """Physical cores `threads` busy threads occupy at most on this host's
+    affinity set (the scheduler spreads them over cores before SMT
+    siblings): min(threads, physical cores in the affinity set)."""
+    phys = _affinity_cores(sorted(os.sched_getaffinity(0)))
+    return min(threads, phys) if phys else threads
+
+
 def cpu_model() -> dict:
-    """CPU model name and physical-core count of this host (/proc/cpuinfo)."""
+    """CPU model name, physical cores (whole host and this process's affinity
+    set) and NUMA nodes of this host."""
     model, phys = "unknown", set()
     try:
         cur = {}
@@ -384,48 +413,63 @@ def cpu_model() -> dict:
                     model = v.strip()
     except OSError:
         pass
+    aff = sorted(os.sched_getaffinity(0))
+    try:
+        numa = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node")
+                    and d[4:].isdigit()])
+    except OSError:
+        numa = None
     return {"model": model, "physical_cores": len(phys) or None,
-            "logical_cpus": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0))}
+            "logical_cpus": os.cpu_count(), "affinity_cpus": len(aff),
+            "affinity_physical_cores": _affinity_cores(aff), "numa_nodes": numa}
 
 
-def baseline_plan(codec: Codec, buf, off, ln, thread_counts, reps: int = 5) -> dict:
+def baseline_plan(codec: Codec, buf, off, ln, thread_counts, reps: int = 5,
+                  partitions=(0,)) -> dict:
     """BASELINE.md "CPU-baseline plan": the codec over the same blocks the GPU
-    timed, once per thread count (static round-robin partition, cpu_batch.c),
-    outputs in pre-faulted buffers reused across runs, one untimed warm-up,
-    then the median of `reps` timed runs, encode and decode separately.
-    Returns per-thread-count GiB/s plus the compressed output (for the
-    byte-for-byte check against the GPU's)."""
+    timed, once per thread count and block partition (cpu_batch.c: 0 static
+    round-robin, 1 contiguous), one untimed warm-up, then the median of
+    `reps` timed runs, encode and decode separately.  The outputs are fresh,
+    untouched buffers for every (threads, partition): the warm-up's worker
+    threads fault their own pages in, so on a multi-socket host each thread
+    writes memory of its own NUMA node (buffers reused from a run with
+    another partition would keep that run's placement), and the timed runs
+    reuse those pre-faulted pages.  Returns GiB/s per (threads, partition)
+    plus the compressed output (for the byte-for-byte check against the
+    GPU's)."""
     n = int(ln.shape[0])
     raw = int(ln.sum(dtype=np.uint64))
     bounds = (ln.astype(np.uint64) * 7 // 6 + 48) // 16 * 16
     ooff = np.zeros(n, dtype=np.uint64)
     if n:
         ooff[1:] = np.cumsum(bounds[:-1])
-    comp = np.ones(int(bounds.sum()) + 16, dtype=np.uint8)       # ones: pre-faulted
-    olen = np.zeros(n, dtype=np.uint32)
     caps64 = (ln.astype(np.uint64) + 15) // 16 * 16
     doff = np.zeros(n, dtype=np.uint64)
     if n:
         doff[1:] = np.cumsum(caps64[:-1])
-    dec = np.ones(int(caps64.sum()) + 16, dtype=np.uint8)
-    st = np.zeros(n, dtype=np.uint8)
-    res = {}
+    res, keep = {}, None
     for t in thread_counts:
-        te, td = [], []
-        for r in range(reps + 1):
-            t0 = time.perf_counter()
-            codec._batch(0, codec.f_encode, t, buf, off, ln, comp, ooff, olen, None)
-            t1 = time.perf_counter()
-            codec._batch(1, codec.f_decode, t, comp, ooff, olen, dec, doff, None, st)
-            t2 = time.perf_counter()
-            if r:                      # run 0 is the warm-up
-                te.append(t1 - t0)
-                td.append(t2 - t1)
-        if not bool((st == 1).all()):
-            raise RuntimeError("CPU baseline: reference decode rejected its own output")
-        e, d = float(np.median(te)), float(np.median(td))
-        res[t] = {"encode_GiBps": raw / e / 2**30, "decode_GiBps": raw / d / 2**30,
-                  "roundtrip_GiBps": raw / (e + d) / 2**30,
-                  "encode_s_median": e, "decode_s_median": d}
-    return {"per_threads": res, "raw_bytes": raw, "comp": (comp, ooff, olen)}
+        for part in (partitions if t > 1 else (0,)):
+            comp = np.empty(int(bounds.sum()) + 16, dtype=np.uint8)    # untouched pages
+            dec = np.empty(int(caps64.sum()) + 16, dtype=np.uint8)
+            olen = np.zeros(n, dtype=np.uint32)
+            st = np.zeros(n, dtype=np.uint8)
+            te, td = [], []
+            for r in range(reps + 1):
+                t0 = time.perf_counter()
+                codec._batch(0, codec.f_encode, t, buf, off, ln, comp, ooff, olen, None, part)
+                t1 = time.perf_counter()
+                codec._batch(1, codec.f_decode, t, comp, ooff, olen, dec, doff, None, st, part)
+                t2 = time.perf_counter()
+                if r:                      # run 0 is the warm-up
+                    te.append(t1 - t0)
+                    td.append(t2 - t1)
+            if not bool((st == 1).all()):
+                raise RuntimeError("CPU baseline: reference decode rejected its own output")
+            e, d = float(np.median(te)), float(np.median(td))
+            res[(t, part)] = {"encode_GiBps": raw / e / 2**30, "decode_GiBps": raw / d / 2**30,
+                              "roundtrip_GiBps": raw / (e + d) / 2**30,
+                              "encode_s_median": e, "decode_s_median": d}
+            keep = (comp, ooff, olen)
+            del dec
+    return {"per_threads": res, "raw_bytes": raw, "comp": keep}

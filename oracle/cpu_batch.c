@@ -3,7 +3,7 @@
  *
  * Drives a per-block CPU codec (the oracle restatement, or the reference
  * snappy.c compiled into oracle/_ref/) over a batch of blocks with a static
- * round-robin block partition across T pthreads.  Used by tests/ to check
+ * round-robin (or contiguous) block partition across T pthreads.  Used by tests/ to check
  * whole corpora and by bench.py's cpu_baseline leg (BASELINE.md "CPU-baseline
  * plan": 1 thread and N threads, round-robin).  The codec is passed in as
  * function pointers with the signatures of lcdb's src/util/snappy.h:31-38.
@@ -28,7 +28,7 @@ typedef struct {
   const uint64_t *out_off;
   uint32_t *out_len;         /* encode: bytes written; decode: unused */
   uint8_t *status;           /* decode: 1 ok / 0 corrupt; may be NULL */
-  uint32_t n;
+  uint32_t n;               /* blocks [first, n) with this stride */
   uint32_t stride;
   uint32_t first;
 } cb_job;
@@ -54,13 +54,17 @@ cb_worker(void *arg) {
   return NULL;
 }
 
-/* Returns 0 on success, -1 if a thread could not be started. */
+/* partition 0: static round-robin (thread t takes blocks t, t + T, ...);
+ * partition 1: contiguous (thread t takes blocks [t n / T, (t + 1) n / T)),
+ * so each thread's output pages are its own (first-touched by it when the
+ * caller passes untouched buffers).  Returns 0 on success, -1 if a thread
+ * could not be started. */
 int
-cpu_batch_run(int mode, void *fn, int threads,
-              const uint8_t *in, const uint64_t *in_off,
-              const uint32_t *in_len, uint8_t *out,
-              const uint64_t *out_off, uint32_t *out_len,
-              uint8_t *status, uint32_t n) {
+cpu_batch_run2(int mode, void *fn, int threads, int partition,
+               const uint8_t *in, const uint64_t *in_off,
+               const uint32_t *in_len, uint8_t *out,
+               const uint64_t *out_off, uint32_t *out_len,
+               uint8_t *status, uint32_t n) {
   pthread_t *tid;
   cb_job *jobs;
   int t, rc = 0;
@@ -89,9 +93,15 @@ cpu_batch_run(int mode, void *fn, int threads,
     j->out_off = out_off;
     j->out_len = out_len;
     j->status = status;
-    j->n = n;
-    j->stride = (uint32_t)threads;
-    j->first = (uint32_t)t;
+    if (partition == 1) {
+      j->first = (uint32_t)((uint64_t)n * (uint64_t)t / (uint64_t)threads);
+      j->n = (uint32_t)((uint64_t)n * (uint64_t)(t + 1) / (uint64_t)threads);
+      j->stride = 1;
+    } else {
+      j->n = n;
+      j->stride = (uint32_t)threads;
+      j->first = (uint32_t)t;
+    }
   }
 
   if (threads == 1) {
@@ -112,4 +122,14 @@ cpu_batch_run(int mode, void *fn, int threads,
   free(tid);
   free(jobs);
   return rc;
+}
+
+int
+cpu_batch_run(int mode, void *fn, int threads,
+              const uint8_t *in, const uint64_t *in_off,
+              const uint32_t *in_len, uint8_t *out,
+              const uint64_t *out_off, uint32_t *out_len,
+              uint8_t *status, uint32_t n) {
+  return cpu_batch_run2(mode, fn, threads, 0, in, in_off, in_len, out, out_off,
+                        out_len, status, n);
 }

@@ -46,6 +46,15 @@ def test_library_exports_every_declared_symbol():
         assert getattr(lib, name) is not None
 
 
+def test_library_exports_only_the_c_abi():
+    # The library is loaded into lcdb's process: nothing but the drop-in
+    # (ldb_snappy_*) and the batched ABI (lgs_*) may be exported, so no
+    # helper can interpose on the host's symbols (lcdb_amd/csrc/exports.map).
+    extra = {s for s in _dynsyms(build.LIB) if not s.startswith(("ldb_snappy_", "lgs_"))}
+    assert not extra, sorted(extra)[:20]
+    assert _dynsyms(build.LIB) == _declared()
+
+
 def test_product_does_not_link_the_oracle():
     syms = _dynsyms(build.LIB)
     assert not any(s.startswith(("oracle_", "cpu_batch")) for s in syms)

@@ -162,3 +162,32 @@ print("ok", len(data), len(enc), fp)
     r = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok"), (r.stdout, r.stderr[-3000:])
+
+
+@pytest.mark.gpu
+def test_dropin_alloc_failure_is_not_corruption(gpu):
+    # a block larger than a drop-in slot takes device memory for
+    # the call; a failed allocation must never come back as 0 (lcdb turns
+    # that into LDB_CORRUPTION, format.c:247-251).  A few failures are
+    # retried and the block decodes; a device that stays out of memory ends
+    # the call loudly (LGS_DIE_EXIT makes that an exit code, not SIGABRT).
+    prog = r'''
+import sys
+sys.path.insert(0, %r)
+import oracle
+from lcdb_amd import corpus, snappy, _native
+data = b"".join(corpus.fillseq(400).blocks())[:(3 << 20) + 77]
+enc = oracle.best().encode(data)
+_native.set_option("inject_alloc_failures", sys.argv[1])
+out = snappy.decode(enc)
+print("decoded", out == data)
+''' % ROOT
+    env = dict(os.environ, LGS_DROPIN_MB="1", LGS_DIE_EXIT="70")
+    r = subprocess.run([sys.executable, "-c", prog, "3"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "decoded True", (r.stdout, r.stderr[-2000:])
+    r = subprocess.run([sys.executable, "-c", prog, "1000"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 70, (r.returncode, r.stdout, r.stderr[-2000:])
+    assert "decoded" not in r.stdout
+    assert "hipMalloc" in r.stderr and "ldb_snappy_decode failed" in r.stderr, r.stderr[-2000:]

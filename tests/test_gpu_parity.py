@@ -473,6 +473,31 @@ def test_decode_wide_far_copies_long_literals_and_rejects(gpu):
             for _ in range(4):
                 k = rng.randrange(1, len(s))
                 streams.append(s[:k] + bytes([rng.randrange(256)]) + s[k + 1:])
+    # Through the drop-in too: outputs of 16 897 - 66 048 bytes
+    # decode in the slot's mapped, coherent pinned memory, so far copies
+    # there read flushed output back across PCIe.
+    small = (_lit(rnd(40000)) + _copy2(64, 40000) + _copy2(64, 33000) + _copy2(20, 32705)
+             + _lit(rnd(100)) + _copy2(60, 40200) + bytes([1 | (6 << 2) | (3 << 5), 0x10])
+             + _lit(rnd(20000)) + _copy2(64, 60000) + _copy2(7, 3) + _copy2(64, 1))
+    smade = 40000 + 64 + 64 + 20 + 100 + 60 + 10 + 20000 + 64 + 7 + 64
+    assert 16896 < smade <= 66048
+    sgood = _varint(smade) + small
+    dropin = [sgood, sgood[:-1], sgood[:len(sgood) // 2], _varint(smade + 1) + small,
+              _varint(smade - 1) + small, _varint(40100) + _lit(rnd(40000)) + _copy2(64, 40001)]
+    for bs, n in ((65536, 2),):
+        for blk in list(corpus.fillseq(n, block_size=bs, key0=7).blocks()) + list(
+                corpus.random_blocks(n, bs, seed=5).blocks()):
+            s = ref.encode(blk)
+            dropin += [s, s[:-3]]
+            for _ in range(3):
+                k = rng.randrange(1, len(s))
+                dropin.append(s[:k] + bytes([rng.randrange(256)]) + s[k + 1:])
+    dok = 0
+    for k, s in enumerate(dropin):
+        exp = ref.decode(s)
+        assert gpu.decode(s) == exp, k
+        dok += exp is not None
+    assert dok >= 5
     caps = [1 << 19] * len(streams)
     res, st = gpu.decode_batch_host(streams, caps)
     oks = 0

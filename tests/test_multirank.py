@@ -141,3 +141,64 @@ def test_oracle_shards_reassemble_to_reference_dd(digests):
         per.append(corpus.block_digests(out, ooff, olen))
     allb = shard.interleave(per, 1024)
     assert corpus.digest_of_digests(allb) == digests["C1_fillseq_1024x4KiB"]["comp_dd"]
+
+
+def test_bench_launcher_fails_fast_when_a_rank_dies():
+    """A rank that exits non-zero ends the launch at once (the survivors are
+    terminated, not left in gloo's rendezvous until its timeout)."""
+    import time
+    t0 = time.perf_counter()
+    r = _bench("--gpus", "2", "--plan-only", "--total-blocks", "-5")
+    assert r.returncode != 0
+    assert time.perf_counter() - t0 < 120
+
+
+def test_cpu_baseline_fields_on_cpu():
+    """bench.py's cpu_baseline leg (no GPU needed): 1 thread, the per-GPU
+    share and nproc threads, both partitions, the reference's bytes."""
+    import argparse
+
+    import bench
+    from lcdb_amd import corpus
+    c = corpus.fillseq(256)
+    a = argparse.Namespace(cpu_threads=2, cpu_sample=256, cpu_reps=1)
+    out, ooff, olen = oracle.best().encode_batch(c.buf, c.off, c.len, 1)
+
+    class H:   # the GPU's compressed blocks, as bench.py holds them
+        buf, off, len = out, ooff, olen
+    cb = bench.cpu_baseline(c, a, H, 1)
+    nproc = len(os.sched_getaffinity(0))
+    assert cb["threads"] == nproc and cb["nproc"]["threads"] == nproc
+    assert cb["single_thread"]["threads"] == 1 and cb["per_gpu_share"]["threads"] == 2
+    assert 1 <= cb["cores"] <= nproc
+    assert cb["same_bytes_as_gpu"] is True
+    assert cb["value"] == cb["nproc"]["roundtrip_GiBps"] > 0
+    if nproc > 1:
+        assert set(cb["nproc"]["by_partition"]) == {"round-robin", "contiguous"}
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_the_gpu_c2(digests):
+    """bench.py --gpus 2 on the GPU box (the ranks share its GPU): C2's 65 536
+    blocks dealt g -> g % 2, every rank encodes and decodes its shard, and
+    rank 0's re-interleaved per-block digests equal the pinned C2 comp_dd."""
+    r = _bench("--gpus", "2", "--total-blocks", "65536", "--steps", "2", "--warmup", "1",
+               "--no-c3", "--no-cpu-baseline", "--no-pipelined", "--no-copy-probe")
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["config"]["blocks_rank0"] == 32768
+    assert line["parity"].startswith("compressed blocks == reference (C2_fillseq_65536x4KiB")
+    assert len(line["per_rank_elapsed_s"]["ranks"]) == 2
+
+
+@pytest.mark.gpu
+def test_bench_c4_full_stream_on_one_gpu(digests):
+    """C4 (BASELINE.json configs[3]): the whole 1 048 576-block stream encoded
+    and decoded on one GPU; compressed blocks equal the pinned C4 comp_dd."""
+    r = _bench("--gpus", "1", "--total-blocks", "1048576", "--steps", "1", "--warmup", "1",
+               "--copies", "1", "--no-c3", "--no-cpu-baseline", "--no-pipelined",
+               "--no-copy-probe")
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["config"]["workload"].startswith("C4:")
+    assert line["parity"].startswith("compressed blocks == reference (C4_fillseq_1048576x4KiB")

@@ -14,8 +14,10 @@ srcs="lgs_api.cpp lgs_encode.hip lgs_decode.hip lgs_table.hip lgs_bloom.hip lgs_
 build() {   # $1: source root, $2: output
   local args=()
   for s in $srcs; do args+=("$1/lcdb_amd/csrc/$s"); done
+  local map=()
+  [ -f "$1/lcdb_amd/csrc/exports.map" ] && map=("-Wl,--version-script=$1/lcdb_amd/csrc/exports.map")
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -pthread \
-    -I"$1/include" "${args[@]}" -o "$2" "${@:3}"
+    -I"$1/include" "${map[@]}" "${args[@]}" -o "$2" "${@:3}"
 }
 build "$tmp" probes/base.so &
 build "$PWD" probes/new.so &
