@@ -727,6 +727,7 @@ Options& options_init() {
     const char* dk = getenv("LGS_DECODE_KERNEL");
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
+    if (dk && !strcmp(dk, "quad")) v->decoder = kDecQuad;
     const char* ns = getenv("LGS_NO_SPLIT");
     if (ns && *ns && strcmp(ns, "0")) v->split = 0;
     return v;
@@ -800,7 +801,8 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
+    else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring, quad or wave)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)

@@ -1000,10 +1000,15 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     if (take & far) {
       // Flushed already: it ends <= made - kNear + 64 < F.
       const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
+#ifndef LGS_PROBE_NOFAR
       fa0 = ld16(sp);
       if (orem > 16) fa1 = ld16(sp + 16);
       if (orem > 32) fa2 = ld16(sp + 32);
       if (orem > 48) fa3 = ld16(sp + 48);
+#else
+      (void)sp;
+      fa0 = fa1 = fa2 = fa3 = u32x4{0, 0, 0, 0};
+#endif
     }
   };
 
@@ -1073,8 +1078,12 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
                                 ((jb.off + 16 * w) & (kOutRing - 1)));
           const gptr<uint8_t> g =
               (gptr<uint8_t>)jb.ptr() + jb.off + 16 * w;
+#ifndef LGS_PROBE_NOFLUSH
           if (16 * w + 16 <= jb.cnt) st16(g, v);
           else st_exact(g, v, jb.cnt - 16 * w);
+#else
+          if (v.x == 0x12345678u && jb.cnt == 77777u) st16(g, v);   // (never: keeps v live)
+#endif
         }
       }
       order();
@@ -1141,8 +1150,406 @@ hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
   // 20 KB of LDS, so eight waves fit a CU, two per SIMD, and each hides the
   // other's memory waits.  (64 blocks per wave: 746 -> 709 GiB/s on C2; one
   // op slot: 632.  Those variants were removed in round 2.)
-  hipLaunchKernelGGL((decode_ring_kernel<true, 32>), dim3((a.n + 31) / 32), dim3(64), 0, s, a.in,
+#ifndef LGS_RING_BL
+#define LGS_RING_BL 32
+#endif
+  hipLaunchKernelGGL((decode_ring_kernel<true, LGS_RING_BL>), dim3((a.n + LGS_RING_BL - 1) / LGS_RING_BL), dim3(64), 0, s, a.in,
                      a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
+                     a.index, a.n, a.count);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Quad decoder: four lanes per block, up to four consecutive ops per trip.
+//
+// The ring decoder above is bound by its per-wave instruction stream: one
+// lane walks each block, so a wave's life is ~110 trips of ~560 dependent
+// instructions whatever the lane count (profiles/r3e_ringprobe.txt: dropping
+// every flush store and far-copy load moves it by < 5 %).  Here the four
+// lanes of a DPP quad own one block (16 blocks per wave, 16 waves per CU
+// for C2) and a trip takes the block's next ops as far as four tags, 128
+// output bytes, the landed input and one far copy go:
+//   * parse: the quad's lanes walk the four tags together (identical work on
+//     each lane, no cross-lane traffic); lane g keeps tag g.  Every reject
+//     of snappy.c:216-338 is checked in the reference's order (parse_tag).
+//   * a copy whose source lies inside the trip's last literal reads that
+//     literal's bytes from the input ring (no dependency on this trip's
+//     writes); a copy reading other bytes this trip writes waits a round
+//     (all lower slots written first; ~6 % of trips need one).
+//   * every round reads all of its sources before it writes (reads-first),
+//     and writes exactly the op's bytes (16-byte chunks + an 8/4/2/1 tail),
+//     so ops of one round never clobber each other or the near window.
+//   * a far copy (beyond the 240-byte near window) is the trip's one load:
+//     the quad fetches its <= 64 bytes from the flushed output, 16 a lane,
+//     and they land at the start of the next trip; later ops of the trip go
+//     on unless they read them.
+//   * flushes and refills are the quad's own 16-byte lanes: 64 contiguous
+//     bytes per instruction per block, no job records.
+// So a block takes ~50 trips instead of ~110, each of a similar number of
+// instructions for four times as many lanes of useful work.
+// ---------------------------------------------------------------------------
+namespace quad {
+constexpr uint32_t kIR = 128, kIS = 208;     // input ring; stride (ring + 64 mirror + 16 sink)
+constexpr uint32_t kOR = 256, kOS = 352;     // output ring; stride (16 pad + ring + 64 mirror + 16 sink)
+constexpr uint32_t kNear = 240;               // ring minus one 16-byte granule of slack
+constexpr uint32_t kBudget = 128;             // output bytes per block and trip
+constexpr uint32_t kBW = 16;                  // blocks per wave
+}  // namespace quad
+
+// Exact-size LDS writes of the first t < 16 bytes of v at p (8/4/2/1-byte
+// pieces; lanes that skip a piece aim it at their sink).
+__device__ __forceinline__ void lds_tail(uint8_t* p, u32x4 v, uint32_t t, uint8_t* sink) {
+  typedef uint64_t u64_a1 __attribute__((aligned(1)));
+  typedef uint32_t u32_a1 __attribute__((aligned(1)));
+  typedef uint16_t u16_a1 __attribute__((aligned(1)));
+  uint8_t* q = p;
+  *(u64_a1*)((t & 8) ? q : sink) = ((uint64_t)v.y << 32) | v.x;
+  if (t & 8) v = u32x4{v.z, v.w, 0, 0};
+  q += t & 8;
+  *(u32_a1*)((t & 4) ? q : sink) = v.x;
+  if (t & 4) v.x = v.y;
+  q += t & 4;
+  *(u16_a1*)((t & 2) ? q : sink) = (uint16_t)v.x;
+  if (t & 2) v.x >>= 16;
+  q += t & 2;
+  *((t & 1) ? q : sink) = (uint8_t)v.x;
+}
+
+// Write n <= 64 bytes (c0..c3 = bytes 0..63) at output position at of a
+// quad lane's output ring ob: whole 16-byte chunks, then the exact tail,
+// each also into the mirror (ring offsets < 64) or the pre-pad (pieces that
+// wrap past 256) so any read of <= 64 bytes at a ring offset is linear.
+__device__ __forceinline__ void qo_put(uint8_t* ob, uint32_t at, uint32_t n, u32x4 c0, u32x4 c1,
+                                       u32x4 c2, u32x4 c3, uint8_t* sink) {
+  using namespace quad;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const u32x4 v = k == 0 ? c0 : (k == 1 ? c1 : (k == 2 ? c2 : c3));
+    const uint32_t r = (at + 16 * k) & (kOR - 1);
+    if (16 * k + 16 <= n) {
+      lwr16(ob + r, v);
+      if (r - 64 > 176u) lwr16(ob + (int32_t)r + (r < 64 ? 256 : -256), v);
+    } else if (16 * k < n) {
+      const uint32_t t = n - 16 * k;
+      lds_tail(ob + r, v, t, sink);
+      // the mirror copy of the tail: ring offsets < 64 also at +256, a tail
+      // running past 256 also at -256 (the pre-pad holds offsets -16..-1)
+      const bool mir = (r < 64) | (r + t > kOR);
+      lds_tail(mir ? ob + (int32_t)r + (r < 64 ? 256 : -256) : sink, v, mir ? t : 0u, sink);
+    }
+  }
+}
+
+// Bytes [b0, b1) of the 16-byte value v to p + b0 .. p + b1 - 1 (global),
+// one byte store each (inline asm: see st_exact).
+__device__ __forceinline__ void st_range(gptr<uint8_t> p, u32x4 v, uint32_t b0, uint32_t b1) {
+#pragma clang loop unroll(disable) vectorize(disable) interleave(disable)
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t byte = byte_of(v, b);
+    asm volatile("global_store_byte %0, %1, off\n\ts_nop 1" ::"v"(p + b), "v"(byte) : "memory");
+  }
+}
+
+// 16 bytes at stream position p of a quad's input ring (linear through the
+// mirror for reads of <= 64 bytes).
+__device__ __forceinline__ u32x4 qi_get(const uint8_t* ib, uint32_t p) {
+  return lrd16(ib + (p & (quad::kIR - 1)));
+}
+
+__global__ __launch_bounds__(64) void decode_quad_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
+  using namespace quad;
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[kBW * kIS];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kBW * kOS];
+
+  const uint32_t lane = threadIdx.x;
+  const uint32_t qb = lane >> 2, g = lane & 3u;      // block in the wave, slot in the quad
+  const uint32_t slot = blockIdx.x * kBW + qb;
+  if (count) n = *count;
+  if (blockIdx.x * kBW >= n) return;                // a whole wave without blocks
+  const bool exists = slot < n;
+  const uint32_t i = exists ? (index ? index[slot] : slot) : 0;
+  const gptr<const uint8_t> src = to_global(in) + (exists ? in_off[i] : 0);
+  const uint32_t slen = exists ? in_len[i] : 0;
+  const gptr<uint8_t> dst = to_global(out) + (exists ? out_off[i] : 0);
+  const uint32_t cap = exists ? out_cap[i] : 0;
+  uint8_t* const ib = s_in + qb * kIS;
+  uint8_t* const ob = s_out + qb * kOS + 16;
+  uint8_t* const osink = ob + kOR + 64;
+
+  // varint32 header, coding.h:169-204.  st: 1 decoding/ok, 0 corrupt, 2 no
+  // space, 3 no block.
+  uint32_t st = exists ? 1u : 3u, want = 0, hlen = 0;
+  if (exists) {
+    const uint64_t h = view8(src);
+    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
+      const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
+      if ((b & 0x80u) == 0) {
+        want |= b << (7 * k);
+        hlen = k + 1;
+        break;
+      }
+      want |= (b & 0x7fu) << (7 * k);
+    }
+    if (hlen == 0 || want > 0x7fffffffu) st = 0;                // snappy.c:405-409
+    else if (want > cap) st = 2;
+  }
+
+  // Prologue: the stream's first 128 bytes (two 16-byte granules a lane).
+  uint32_t in_req = 0, in_have = 0;
+  {
+    u32x4 a = {0, 0, 0, 0}, b = a;
+    const uint32_t o0 = 16 * g, o1 = 64 + 16 * g;
+    if ((st == 1) & (o0 < slen)) a = ld16(src + o0);
+    if ((st == 1) & (o1 < slen)) b = ld16(src + o1);
+    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+    lwr16(ib + o0, a);
+    lwr16(ib + o1, b);
+    lwr16(ib + kIR + o0, a);                                    // mirror of offsets 0..63
+    order();
+    in_req = in_have = st == 1 ? (slen < kIR ? slen : kIR) : 0u;
+  }
+
+  uint32_t pos = hlen;               // next tag (stream offset)
+  uint32_t made = 0, F = 0;          // output produced / flushed
+  uint32_t orem = 0, olp = 0;        // a long literal's bytes left / their stream position
+  // The far copy in flight: its output position and length (quad-uniform),
+  // and this lane's 16 bytes of it.
+  uint32_t fat = 0, flen = 0;
+  u32x4 fv = {0, 0, 0, 0};
+  // Refills in flight: up to two 16-byte granules a lane, their ring offsets
+  // (0xffffffff: none).
+  u32x4 rv0 = fv, rv1 = fv;
+  uint32_t ra0 = 0xffffffffu, ra1 = 0xffffffffu;
+  const uint64_t dpa = reinterpret_cast<uint64_t>(dst);
+  const uint32_t dsh = (uint32_t)(dpa & 15u);
+
+  for (;;) {
+    // ---- everything issued last trip has landed: the far copy's bytes, then
+    // the refills.
+    __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+    if (flen > 0) {
+      const u32x4 z = {0, 0, 0, 0};
+      const uint32_t k0 = 16 * g;
+      if (k0 < flen) qo_put(ob, fat + k0, flen - k0 < 16 ? flen - k0 : 16u, fv, z, z, z, osink);
+      flen = 0;
+    }
+    if (ra0 != 0xffffffffu) {
+      lwr16(ib + ra0, rv0);
+      if (ra0 < 64) lwr16(ib + kIR + ra0, rv0);
+    }
+    if (ra1 != 0xffffffffu) {
+      lwr16(ib + ra1, rv1);
+      if (ra1 < 64) lwr16(ib + kIR + ra1, rv1);
+    }
+    ra0 = ra1 = 0xffffffffu;
+    in_have = in_req;
+    order();
+
+    // ---- flush: whole 64-byte segments of the destination up to made, the
+    // block's tail once its stream is consumed (snappy.c:337: it must end
+    // exactly at want).
+    if ((st == 1) & (orem == 0) & (pos >= slen) & (made != want)) st = 0;
+    const bool fin = (st == 1) & (orem == 0) & (pos >= slen);
+    {
+      const uint64_t lb = (dpa + made) & ~(uint64_t)63;
+      const uint32_t lim = lb > dpa ? (uint32_t)(lb - dpa) : 0u;
+      const uint32_t T = (st != 1) ? F : (fin ? made : (lim > F ? lim : F));
+      if (ballot(T > F)) {
+        const uint32_t g0 = (F + dsh) >> 4, g1 = (T + dsh + 15) >> 4;
+        const gptr<uint8_t> A = dst - dsh;                       // 16-byte aligned
+#pragma clang loop unroll(disable)
+        for (uint32_t j = g0 + g; ballot(j < g1); j += 4) {
+          if (j < g1) {
+            const uint32_t lo = 16 * j - dsh;                    // output position
+            const u32x4 v = lrd16(ob + (lo & (kOR - 1)));
+            if ((16 * j >= F + dsh) & (16 * j + 16 <= T + dsh)) {
+              st16(A + 16 * j, v);
+            } else {
+              // the block's first or last granule: only bytes [F, T)
+              const uint32_t b0 = F + dsh > 16 * j ? F + dsh - 16 * j : 0u;
+              const uint32_t b1 = T + dsh < 16 * j + 16 ? T + dsh - 16 * j : 16u;
+              st_range(A + 16 * j, v, b0, b1);
+            }
+          }
+        }
+      }
+      F = T;
+    }
+    const bool active = (st == 1) & !(fin & (F >= made));
+    if (ballot(active) == 0) break;
+
+    // ---- parse: up to four tags, the quad's lanes walking them together.
+    uint32_t my_n = 0, my_src = 0, my_at = 0, my_kind = 0, my_dist = 0;
+    // kinds: 0 input ring (literal, or a copy of this trip's literal),
+    // 1 output ring, 2 far (global), 3 overlapping copy (dist < n)
+    bool my_dep = false;
+    const uint32_t made0 = made;
+    bool has_far = false;
+    uint32_t far_src = 0;
+    if (active & (orem > 0)) {
+      // a long literal's next piece, in slot 0 only
+      const uint32_t pc = orem < 64 ? orem : 64u;
+      if (olp + pc <= in_have) {
+        if (g == 0) {
+          my_n = pc;
+          my_src = olp;
+          my_at = made;
+          my_kind = 0;
+        }
+        made += pc;
+        orem -= pc;
+        olp += pc;
+      }
+    } else {
+      bool go = active & (pos < slen);
+      uint32_t p = pos, m = made;
+      uint32_t lm0 = 0, lm1 = 0, lw = 0;                         // the trip's last literal
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        if (ballot(go) == 0) break;
+        const uint32_t hneed = slen - p < 5 ? slen : p + 5;
+        go = go & (p < slen) & (in_have >= hneed);
+        const Tag t = parse_tag(qi_get(ib, p), p, slen, want, m);
+        const bool lit = t.kind == 0;
+        const bool longl = lit & (t.len > 64);
+        const uint32_t pc = longl ? 64u : t.len;
+        const uint32_t lp = p + t.hl;                           // a literal's first byte
+        const uint32_t cs = m - t.dist;                         // a copy's first source byte
+        const bool far = !lit & (t.dist > kNear + (m - made0));
+        const bool remap = !lit & (cs >= lm0) & (cs + t.len <= lm1);
+        const bool hits_far = !lit & has_far & (cs < fat + flen) & (cs + t.len > fat);
+        if (go & t.bad) st = 0;
+        const bool take = go & !t.bad & (!lit | (lp + pc <= in_have)) &
+                          ((k == 0) | (m + pc - made0 <= kBudget)) & !(far & has_far) &
+                          !hits_far & !(longl & (k > 0));
+        if (take & (g == k)) {
+          my_n = pc;
+          my_at = m;
+          my_dist = t.dist;
+          my_kind = lit ? 0u : (far ? 2u : (remap ? 0u : (t.dist < t.len ? 3u : 1u)));
+          my_src = lit ? lp : (remap ? lw + (cs - lm0) : cs);
+          my_dep = !lit & !far & !remap & (cs + (t.dist < t.len ? t.dist : t.len) > made0);
+        }
+        if (take & far) {
+          has_far = true;
+          fat = m;
+          flen = t.len;
+          far_src = cs;
+        }
+        if (take & lit) {
+          lm0 = m;
+          lm1 = m + pc;
+          lw = lp;
+        }
+        if (take & longl) {
+          orem = t.len - 64;
+          olp = lp + 64;
+        }
+        p = take ? (longl ? t.next : t.next) : p;
+        m = take ? m + pc : m;
+        go = take & !longl;
+      }
+      pos = p;
+      made = m;
+    }
+
+    // ---- move the bytes: rounds of reads-then-writes.  An op that reads
+    // bytes this trip writes waits until every lower slot of its quad is done.
+    {
+      bool pend = (my_n > 0) & (my_kind != 2u);
+      bool done = !pend;
+#pragma clang loop unroll(disable)
+      for (;;) {
+        const uint64_t dm = ballot(done);
+        const uint32_t qm = (uint32_t)(dm >> (lane & ~3u)) & 0xfu;
+        const uint32_t low = (1u << g) - 1u;
+        const bool ready = pend & (!my_dep | ((qm & low) == low));
+        if (ballot(ready) == 0) break;
+        u32x4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+        if (ready) {
+          if (my_kind == 3u) {
+            // dist < n: the dist bytes before my_at repeat (snappy.c:329-330)
+            const uint32_t d = my_dist;
+            if ((d <= 8) & ((d & (d - 1)) == 0)) {
+              const u32x4 s0 = lrd16(ob + ((my_at - d) & (kOR - 1)));
+              const uint32_t b0 = s0.x & 0xffu, h0 = s0.x & 0xffffu;
+              const uint32_t px = d == 1 ? b0 * 0x01010101u : (d == 2 ? h0 | (h0 << 16) : s0.x);
+              const uint32_t py = d == 8 ? s0.y : px;
+              c0 = c1 = c2 = c3 = u32x4{px, py, px, py};
+            }
+          } else {
+            const uint8_t* sp = my_kind == 0u ? ib + (my_src & (kIR - 1))
+                                              : ob + (my_src & (kOR - 1));
+            c0 = lrd16(sp);
+            if (my_n > 16) c1 = lrd16(sp + 16);
+            if (my_n > 32) c2 = lrd16(sp + 32);
+            if (my_n > 48) c3 = lrd16(sp + 48);
+          }
+        }
+        order();
+        // other periods < 16 (never in fillseq): byte by byte below
+        const bool slow = ready & (my_kind == 3u) & !((my_dist <= 8) & ((my_dist & (my_dist - 1)) == 0));
+        if (ready & !slow) qo_put(ob, my_at, my_n, c0, c1, c2, c3, osink);
+        if (slow) {
+#pragma clang loop unroll(disable)
+          for (uint32_t b = 0; b < my_n; ++b) {
+            const uint8_t v = ob[(my_at + b - my_dist) & (kOR - 1)];
+            order();
+            const uint32_t r = (my_at + b) & (kOR - 1);
+            ob[r] = v;
+            if (r < 64) ob[r + kOR] = v;
+            order();
+          }
+        }
+        order();
+        done = done | ready;
+        pend = pend & !ready;
+      }
+    }
+
+    // ---- the far copy's bytes, 16 a lane, from the flushed output (they end
+    // before made0 - 176 < F): they land at the start of the next trip.
+    if (has_far) {
+      const uint32_t k0 = 16 * g;
+      if (k0 < flen) fv = ld16((gptr<const uint8_t>)(dst + far_src + k0));
+    }
+
+    // ---- refills: the next 64 stream bytes once the 64 they overwrite in the
+    // ring are consumed; up to two a trip.
+    {
+      const uint32_t cons = orem > 0 ? olp : pos;
+      const bool r0 = (st == 1) & (in_req < slen) & (in_req <= cons + 64);
+      if (r0) {
+        const uint32_t o = in_req + 16 * g;
+        if (o < slen) rv0 = ld16(src + o);
+        ra0 = o & (kIR - 1);
+        in_req += 64;
+      }
+      const bool r1 = r0 & (in_req < slen) & (in_req <= cons + 64);
+      if (r1) {
+        const uint32_t o = in_req + 16 * g;
+        if (o < slen) rv1 = ld16(src + o);
+        ra1 = o & (kIR - 1);
+        in_req += 64;
+      }
+    }
+  }
+
+  if (exists & (g == 0)) {
+    status[i] = (uint8_t)st;
+    out_len[i] = st == 1 ? want : 0;
+  }
+}
+
+hipError_t launch_decode_quad(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(decode_quad_kernel, dim3((a.n + quad::kBW - 1) / quad::kBW), dim3(64), 0, s,
+                     a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
                      a.index, a.n, a.count);
   return hipGetLastError();
 }
@@ -1280,6 +1687,7 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (force == kDecAuto && !a.index && max_out > kDecCap0 && a.n >= kSplitMinBlocks &&
       options().split.load(std::memory_order_relaxed))
     return launch_decode_split(a, max_out, s);
+  if (force == kDecQuad) return launch_decode_quad(a, s);
   if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))
     return launch_decode_ring(a, s);
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);

@@ -14,7 +14,7 @@ namespace lgs {
 // Process-wide kernel choices (lgs_set_option; the initial values come from
 // LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
 // launch path reads the environment).
-enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2 };
+enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3 };
 struct Options {
   std::atomic<int> decoder{kDecAuto};   // DecodeKernel
   std::atomic<int> split{1};            // size-class split of mixed batches

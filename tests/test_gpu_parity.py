@@ -197,7 +197,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "ring"])
+@pytest.mark.parametrize("kernel", ["wave", "ring", "quad"])
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -224,7 +224,7 @@ def test_decode_kernels_c2_full_size(gpu, digests, force):
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
-    for kernel in ("ring", "wave"):
+    for kernel in ("ring", "wave", "quad"):
         force("decoder", kernel)
         out = batch.decode_slots(c.len)
         st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
@@ -291,14 +291,15 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force):
+@pytest.mark.parametrize("kernel", ["ring", "quad"])
+def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
     # slots at odd offsets (flushes that are not line aligned, byte-exact
     # block ends next to the neighbouring block).
     import torch
     from lcdb_amd import batch
-    force("decoder", "ring")
+    force("decoder", kernel)
     d = digests["C3_mixed"]
     c = corpus.mixed()
     raw = batch.upload(c)
@@ -352,7 +353,7 @@ def _runahead_stream(want: int, copy_frac: float) -> bytes:
     return bytes(s)
 
 
-@pytest.mark.parametrize("kernel", [None, "ring"])
+@pytest.mark.parametrize("kernel", [None, "ring", "quad"])
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.

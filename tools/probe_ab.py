@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of probe builds of the codec library on C2 (timing only).
 
-usage: python tools/probe_ab.py LIB [LIB ...]
+usage: python tools/probe_ab.py LIB[@DECODER] [LIB[@DECODER] ...]
 Each LIB (a .so built from the same sources with a probe macro, e.g.
 -DLGS_PROBE_ALIGNED_RING) runs in its own process: C2 encode and decode,
 3 warm-up + 20 timed launches each, HIP events on the launch stream.
@@ -33,7 +33,8 @@ def child(lib: str) -> None:
     out = batch.decode_slots(c.len)
     st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
-    res = {"lib": os.path.basename(lib)}
+    res = {"lib": os.path.basename(lib) + (("@" + os.environ["LGS_DECODE_KERNEL"])
+                                           if os.environ.get("LGS_DECODE_KERNEL") else "")}
     for name, fn in (("encode", lambda: batch.encode(raw, comp, s)),
                      ("decode", lambda: batch.decode(comp, out, st, s))):
         ts = []
@@ -63,9 +64,12 @@ def main() -> None:
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    for lib in sys.argv[1:]:
+    for spec in sys.argv[1:]:
+        # LIB or LIB@DECODER (LGS_DECODE_KERNEL for that child: ring, quad, wave)
+        lib, _, dk = spec.partition("@")
+        env = dict(os.environ, **({"LGS_DECODE_KERNEL": dk} if dk else {}))
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", lib],
-                           capture_output=True, text=True, timeout=300)
+                           capture_output=True, text=True, timeout=300, env=env)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
         print(line[-1] if line else f"{lib}: rc={r.returncode} {r.stderr[-800:]}", flush=True)
         if r.returncode != 0:
