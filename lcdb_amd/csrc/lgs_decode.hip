@@ -1256,6 +1256,43 @@ __device__ __forceinline__ u32x4 qi_get(const uint8_t* ib, uint32_t p) {
   return lrd16(ib + (p & (quad::kIR - 1)));
 }
 
+// A 16-byte ring write of the lanes with `on`, plus its mirror copy (ring
+// offsets < 64 also at +256, a write running past 256 also at -256), so
+// reads of <= 64 bytes at any ring offset are linear.  Exec-masked, not
+// aimed at a sink: an LDS store costs by the lanes it moves, and sink
+// stores doubled the quad decoder's LDS traffic (419 against 315 us on C2).
+__device__ __forceinline__ void qo_put16(uint8_t* ob, uint32_t at, u32x4 v, bool on, uint8_t*) {
+  const uint32_t r = at & (quad::kOR - 1);
+  if (on) {
+    lwr16(ob + r, v);
+    if (r - 64 > 176u) lwr16(ob + (int32_t)r + (r < 64 ? 256 : -256), v);   // r < 64 or r > 240
+  }
+}
+
+// The trip's independent ops (round one): every source chunk was read
+// before any write (reads-first), so ops of one round never read each
+// other's bytes.  Chunks 3, 2, 1 are written whole even past the op's end
+// (their spill lies inside the next op's first 16 bytes, or past the trip's
+// output), then every op's first 16 bytes exactly (a whole chunk, or the
+// 8/4/2/1-byte pieces of an op under 16 bytes), which rewrites any spill.
+// Spill past the trip's end only touches output not yet made and, in the
+// ring, bytes older than the 240-byte near window.
+__device__ __forceinline__ void qo_put_round1(uint8_t* ob, uint32_t at, uint32_t n, bool on,
+                                              u32x4 c0, u32x4 c1, u32x4 c2, u32x4 c3,
+                                              uint8_t* sink) {
+  using namespace quad;
+  if (ballot(on & (n > 48))) qo_put16(ob, at + 48, c3, on & (n > 48), sink);
+  if (ballot(on & (n > 32))) qo_put16(ob, at + 32, c2, on & (n > 32), sink);
+  if (ballot(on & (n > 16))) qo_put16(ob, at + 16, c1, on & (n > 16), sink);
+  qo_put16(ob, at, c0, on & (n >= 16), sink);
+  const bool sh = on & (n < 16);
+  if (sh) {
+    const uint32_t r = at & (kOR - 1);
+    lds_tail(ob + r, c0, n, sink);
+    if ((r < 64) | (r + n > kOR)) lds_tail(ob + (int32_t)r + (r < 64 ? 256 : -256), c0, n, sink);
+  }
+}
+
 __global__ __launch_bounds__(64) void decode_quad_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
@@ -1269,6 +1306,7 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
 
   const uint32_t lane = threadIdx.x;
   const uint32_t qb = lane >> 2, g = lane & 3u;      // block in the wave, slot in the quad
+  const uint32_t qs = lane & ~3u;                    // the quad's first lane
   const uint32_t slot = blockIdx.x * kBW + qb;
   if (count) n = *count;
   if (blockIdx.x * kBW >= n) return;                // a whole wave without blocks
@@ -1280,6 +1318,7 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
   const uint32_t cap = exists ? out_cap[i] : 0;
   uint8_t* const ib = s_in + qb * kIS;
   uint8_t* const ob = s_out + qb * kOS + 16;
+  uint8_t* const isink = ib + kIR + 64;             // 16 bytes per lane quad: harmless writes
   uint8_t* const osink = ob + kOR + 64;
 
   // varint32 header, coding.h:169-204.  st: 1 decoding/ok, 0 corrupt, 2 no
@@ -1318,36 +1357,34 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
   uint32_t pos = hlen;               // next tag (stream offset)
   uint32_t made = 0, F = 0;          // output produced / flushed
   uint32_t orem = 0, olp = 0;        // a long literal's bytes left / their stream position
-  // The far copy in flight: its output position and length (quad-uniform),
-  // and this lane's 16 bytes of it.
+  // The far copy in flight (in the lane whose slot took it): its output
+  // position and length, and its <= 64 bytes.
   uint32_t fat = 0, flen = 0;
-  u32x4 fv = {0, 0, 0, 0};
-  // Refills in flight: up to two 16-byte granules a lane, their ring offsets
-  // (0xffffffff: none).
-  u32x4 rv0 = fv, rv1 = fv;
-  uint32_t ra0 = 0xffffffffu, ra1 = 0xffffffffu;
+  u32x4 fv0 = {0, 0, 0, 0}, fv1 = fv0, fv2 = fv0, fv3 = fv0;
+  // Refills in flight: up to two 16-byte granules a lane and their ring
+  // offsets (the sink when none).
+  u32x4 rv0 = fv0, rv1 = fv0;
+  uint8_t *ra0 = isink, *ra1 = isink, *rm0 = isink, *rm1 = isink;
   const uint64_t dpa = reinterpret_cast<uint64_t>(dst);
   const uint32_t dsh = (uint32_t)(dpa & 15u);
 
   for (;;) {
-    // ---- everything issued last trip has landed: the far copy's bytes, then
+    // ---- everything issued last trip has landed: the far copy's bytes (the
+    // trip's last op: nothing past it is written yet, so whole chunks), then
     // the refills.
     __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
     if (flen > 0) {
-      const u32x4 z = {0, 0, 0, 0};
-      const uint32_t k0 = 16 * g;
-      if (k0 < flen) qo_put(ob, fat + k0, flen - k0 < 16 ? flen - k0 : 16u, fv, z, z, z, osink);
+      qo_put16(ob, fat, fv0, true, osink);
+      qo_put16(ob, fat + 16, fv1, flen > 16, osink);
+      qo_put16(ob, fat + 32, fv2, flen > 32, osink);
+      qo_put16(ob, fat + 48, fv3, flen > 48, osink);
       flen = 0;
     }
-    if (ra0 != 0xffffffffu) {
-      lwr16(ib + ra0, rv0);
-      if (ra0 < 64) lwr16(ib + kIR + ra0, rv0);
-    }
-    if (ra1 != 0xffffffffu) {
-      lwr16(ib + ra1, rv1);
-      if (ra1 < 64) lwr16(ib + kIR + ra1, rv1);
-    }
-    ra0 = ra1 = 0xffffffffu;
+    if (ra0 != isink) lwr16(ra0, rv0);
+    if (rm0 != isink) lwr16(rm0, rv0);
+    if (ra1 != isink) lwr16(ra1, rv1);
+    if (rm1 != isink) lwr16(rm1, rv1);
+    ra0 = ra1 = rm0 = rm1 = isink;
     in_have = in_req;
     order();
 
@@ -1356,6 +1393,10 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
     // exactly at want).
     if ((st == 1) & (orem == 0) & (pos >= slen) & (made != want)) st = 0;
     const bool fin = (st == 1) & (orem == 0) & (pos >= slen);
+    // Output flushed by earlier trips: their stores were waited for at the
+    // top of this trip, so loads (of other lanes) see it.  A far copy must
+    // read only such bytes (this trip's flush stores are still in flight).
+    const uint32_t F0 = F;
     {
       const uint64_t lb = (dpa + made) & ~(uint64_t)63;
       const uint32_t lim = lb > dpa ? (uint32_t)(lb - dpa) : 0u;
@@ -1384,160 +1425,222 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
     const bool active = (st == 1) & !(fin & (F >= made));
     if (ballot(active) == 0) break;
 
-    // ---- parse: up to four tags, the quad's lanes walking them together.
+    // ---- parse: up to four tags.  The quad's lanes first walk the tag
+    // chain together (identical work on every lane, each tag's length and
+    // step only, snappy.c:210-317's header forms), lane g keeping tag g's
+    // bytes and start; then each lane checks its own tag in full (every
+    // reject of snappy.c:216-338, in the reference's order) and the quad
+    // takes the longest prefix of slots that pass -- at most one far copy or
+    // long literal, as its last.
     uint32_t my_n = 0, my_src = 0, my_at = 0, my_kind = 0, my_dist = 0;
-    // kinds: 0 input ring (literal, or a copy of this trip's literal),
-    // 1 output ring, 2 far (global), 3 overlapping copy (dist < n)
-    bool my_dep = false;
+    // kinds: 0 input ring (a literal, or a copy of the previous slot's
+    // literal), 1 output ring, 2 far (global), 3 overlapping copy (dist < n)
+    bool my_dep = false, my_far = false;
     const uint32_t made0 = made;
-    bool has_far = false;
-    uint32_t far_src = 0;
-    if (active & (orem > 0)) {
+    if (ballot(active & (orem > 0))) {
       // a long literal's next piece, in slot 0 only
       const uint32_t pc = orem < 64 ? orem : 64u;
-      if (olp + pc <= in_have) {
-        if (g == 0) {
-          my_n = pc;
-          my_src = olp;
-          my_at = made;
-          my_kind = 0;
-        }
-        made += pc;
-        orem -= pc;
-        olp += pc;
+      const bool go = active & (orem > 0) & (olp + pc <= in_have);
+      if (go & (g == 0)) {
+        my_n = pc;
+        my_src = olp;
+        my_at = made;
       }
-    } else {
-      bool go = active & (pos < slen);
+      made = go ? made + pc : made;
+      olp = go ? olp + pc : olp;
+      orem = go ? orem - pc : orem;
+    }
+    if (ballot(active & (orem == 0) & (pos < slen))) {
+      const bool live = active & (orem == 0) & (pos < slen) & (made == made0);
       uint32_t p = pos, m = made;
-      uint32_t lm0 = 0, lm1 = 0, lw = 0;                         // the trip's last literal
+      uint32_t my_p = p, my_m = m, my_lo = 0, my_b4 = 0;
 #pragma unroll
       for (uint32_t k = 0; k < 4; ++k) {
-        if (ballot(go) == 0) break;
-        const uint32_t hneed = slen - p < 5 ? slen : p + 5;
-        go = go & (p < slen) & (in_have >= hneed);
-        const Tag t = parse_tag(qi_get(ib, p), p, slen, want, m);
-        const bool lit = t.kind == 0;
-        const bool longl = lit & (t.len > 64);
-        const uint32_t pc = longl ? 64u : t.len;
-        const uint32_t lp = p + t.hl;                           // a literal's first byte
-        const uint32_t cs = m - t.dist;                         // a copy's first source byte
-        const bool far = !lit & (t.dist > kNear + (m - made0));
-        const bool remap = !lit & (cs >= lm0) & (cs + t.len <= lm1);
-        const bool hits_far = !lit & has_far & (cs < fat + flen) & (cs + t.len > fat);
-        if (go & t.bad) st = 0;
-        const bool take = go & !t.bad & (!lit | (lp + pc <= in_have)) &
-                          ((k == 0) | (m + pc - made0 <= kBudget)) & !(far & has_far) &
-                          !hits_far & !(longl & (k > 0));
-        if (take & (g == k)) {
-          my_n = pc;
-          my_at = m;
-          my_dist = t.dist;
-          my_kind = lit ? 0u : (far ? 2u : (remap ? 0u : (t.dist < t.len ? 3u : 1u)));
-          my_src = lit ? lp : (remap ? lw + (cs - lm0) : cs);
-          my_dep = !lit & !far & !remap & (cs + (t.dist < t.len ? t.dist : t.len) > made0);
-        }
-        if (take & far) {
-          has_far = true;
-          fat = m;
-          flen = t.len;
-          far_src = cs;
-        }
-        if (take & lit) {
-          lm0 = m;
-          lm1 = m + pc;
-          lw = lp;
-        }
-        if (take & longl) {
-          orem = t.len - 64;
-          olp = lp + 64;
-        }
-        p = take ? (longl ? t.next : t.next) : p;
-        m = take ? m + pc : m;
-        go = take & !longl;
+        // bytes p .. p+4 from two aligned dwords of the ring (offset p & 127;
+        // the mirror keeps them linear)
+        const uint32_t r = p & (kIR - 1);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(ib + (r & ~3u));
+        const uint32_t w0 = w[0], w1 = w[1];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, r & 3u);
+        const uint32_t b4 = __builtin_amdgcn_alignbyte(0u, w1, r & 3u);   // byte 4 in bits 0..7
+        my_p = g == k ? p : my_p;
+        my_m = g == k ? m : my_m;
+        my_lo = g == k ? lo : my_lo;
+        my_b4 = g == k ? b4 : my_b4;
+        const uint32_t tag = lo & 0xffu, kind = tag & 3u, m0 = tag >> 2;
+        const uint32_t extra = m0 >= 60 ? m0 - 59 : 0u;
+        const uint32_t b1 = (lo >> 8) | (b4 << 24);
+        const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
+        const uint32_t llen = (extra ? (b1 & emask) : m0) + 1;
+        const uint32_t clen = kind == 1 ? 4 + (m0 & 7u) : m0 + 1;
+        const bool lit = kind == 0;
+        p += lit ? 1 + extra + llen : (kind == 3 ? 5u : kind + 1);
+        m += lit ? llen : clen;
       }
-      pos = p;
-      made = m;
+      // this lane's tag, in full (snappy.c:210-324): header form, length,
+      // distance, and the rejects
+      const uint32_t tag = my_lo & 0xffu, kind = tag & 3u, m0 = tag >> 2;
+      const bool lit = kind == 0;
+      const uint32_t extra = (lit & (m0 >= 60)) ? m0 - 59 : 0u;
+      const uint32_t b1 = (my_lo >> 8) | (my_b4 << 24);
+      const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
+      const uint32_t mval = extra ? (b1 & emask) : m0;                 // literal length - 1
+      const uint32_t len = lit ? mval + 1 : (kind == 1 ? 4 + (m0 & 7u) : m0 + 1);
+      const uint32_t hl = lit ? 1 + extra : (kind == 3 ? 5u : kind + 1);
+      const uint32_t dist = kind == 1 ? ((tag & 0xe0u) << 3) | (b1 & 0xffu)
+                                      : (kind == 2 ? b1 & 0xffffu : b1);
+      const uint32_t left = slen - my_p;
+      // :240-256 / :276-317 header in the stream; :263 / :323 length within
+      // want; :258 literal length; :263 literal bytes in the stream; :320 /
+      // :323 0 < dist <= made (dist - 1 >= made also covers dist >= 2^31).
+      const bool bad = (hl > left) | (len > want - my_m) |
+                       (lit ? (mval >= 0x7fffffffu) | (hl + len > left) : (dist - 1 >= my_m));
+      const bool hdr = live & (my_p < slen) & (in_have >= (left < 5 ? slen : my_p + 5));
+      const bool longl = lit & (len > 64);
+      const uint32_t pc = longl ? 64u : len;
+      const uint32_t lp = my_p + hl;                           // a literal's first byte
+      const uint32_t cs = my_m - dist;                         // a copy's first source byte
+      const bool far = !lit & (dist > kNear + (my_m - made0));
+      const bool ok = hdr & !bad & (!lit | (lp + pc <= in_have)) & (!far | (cs + len <= F0)) &
+                      ((g == 0) | (my_m + pc - made0 <= kBudget)) & !(longl & (g > 0));
+      // the longest prefix of passing slots, none after a far copy or a long
+      // literal (quad nibbles of wave ballots)
+      const uint32_t low = (1u << g) - 1u;
+      const uint32_t okm = (uint32_t)(ballot(ok) >> qs) & 0xfu;
+      const uint32_t stopm = (uint32_t)(ballot(ok & (far | longl)) >> qs) & 0xfu;
+      const bool prefix = ((okm & low) == low) & ((stopm & low) == 0);
+      const bool take = ok & prefix;
+      // the first slot that does not pass, with its header in: a reject
+      if ((uint32_t)(ballot(prefix & !ok & hdr & bad) >> qs) & 0xfu) st = 0;
+      const uint32_t nt = (uint32_t)__builtin_popcount((uint32_t)(ballot(take) >> qs) & 0xfu);
+      // a copy that reads the previous slot's literal reads its bytes from
+      // the input ring (no dependency on this trip's writes)
+      const uint32_t pm = __builtin_amdgcn_mov_dpp(my_m, 0x90, 0xf, 0xf, false);    // quad_perm [0,0,1,2]
+      const uint32_t ppc = __builtin_amdgcn_mov_dpp(pc, 0x90, 0xf, 0xf, false);
+      const uint32_t plp = __builtin_amdgcn_mov_dpp(lp, 0x90, 0xf, 0xf, false);
+      const uint32_t plit = __builtin_amdgcn_mov_dpp((uint32_t)lit, 0x90, 0xf, 0xf, false);
+      const bool remap = !lit & (g > 0) & (plit != 0) & (cs >= pm) & (cs + len <= pm + ppc);
+      const bool ovl = !lit & (dist < len);
+      my_n = take ? pc : my_n;
+      my_at = take ? my_m : my_at;
+      my_dist = take ? dist : my_dist;
+      my_far = take & far;
+      my_kind = take ? (lit ? 0u : (far ? 2u : (remap ? 0u : (ovl ? 3u : 1u)))) : my_kind;
+      my_src = take ? (lit ? lp : (remap ? plp + (cs - pm) : cs)) : my_src;
+      // reads bytes this trip writes (or a period that is not 1/2/4/8):
+      // after every lower slot, with exact writes
+      const bool pat = ovl & (dist <= 8) & ((dist & (dist - 1)) == 0);
+      my_dep = take & !lit & !far & !remap &
+               ((cs + (ovl ? dist : len) > made0) | (ovl & !pat));
+      // the block's new position and output: the end of the last taken
+      // slot's tag and op (a long literal: after its first piece; the rest
+      // continues next trip from olp)
+      const uint32_t nxt = my_p + hl + (lit ? len : 0u), mend = my_m + pc;
+      const uint32_t n0 = __builtin_amdgcn_mov_dpp(nxt, 0x00, 0xf, 0xf, false);   // quad_perm [0,0,0,0]
+      const uint32_t n1 = __builtin_amdgcn_mov_dpp(nxt, 0x55, 0xf, 0xf, false);   // [1,1,1,1]
+      const uint32_t n2 = __builtin_amdgcn_mov_dpp(nxt, 0xaa, 0xf, 0xf, false);   // [2,2,2,2]
+      const uint32_t n3 = __builtin_amdgcn_mov_dpp(nxt, 0xff, 0xf, 0xf, false);   // [3,3,3,3]
+      const uint32_t e0 = __builtin_amdgcn_mov_dpp(mend, 0x00, 0xf, 0xf, false);
+      const uint32_t e1 = __builtin_amdgcn_mov_dpp(mend, 0x55, 0xf, 0xf, false);
+      const uint32_t e2 = __builtin_amdgcn_mov_dpp(mend, 0xaa, 0xf, 0xf, false);
+      const uint32_t e3 = __builtin_amdgcn_mov_dpp(mend, 0xff, 0xf, 0xf, false);
+      const uint32_t l0 = __builtin_amdgcn_mov_dpp(len, 0x00, 0xf, 0xf, false);
+      const uint32_t lp0 = __builtin_amdgcn_mov_dpp(lp, 0x00, 0xf, 0xf, false);
+      const bool long0 = (uint32_t)(ballot(take & longl) >> qs) & 1u;
+      const uint32_t nq = nt > 2 ? (nt > 3 ? n3 : n2) : (nt > 1 ? n1 : n0);
+      const uint32_t eq = nt > 2 ? (nt > 3 ? e3 : e2) : (nt > 1 ? e1 : e0);
+      pos = nt ? nq : pos;
+      made = nt ? eq : made;
+      orem = long0 ? l0 - 64 : orem;
+      olp = long0 ? lp0 + 64 : olp;
     }
 
-    // ---- move the bytes: rounds of reads-then-writes.  An op that reads
-    // bytes this trip writes waits until every lower slot of its quad is done.
+    // ---- the far copy's bytes from output flushed by earlier trips (F0),
+    // issued now, landed at the start of the next trip.
+    if (ballot(my_far)) {
+      const gptr<const uint8_t> fp = (gptr<const uint8_t>)(dst + (my_far ? my_src : 0u));
+      if (my_far) {
+        fv0 = ld16(fp);
+        fv1 = ld16(fp + 16);
+        fv2 = ld16(fp + 32);
+        fv3 = ld16(fp + 48);
+      }
+      fat = my_far ? my_at : fat;
+      flen = my_far ? my_n : 0u;
+    }
+
+    // ---- move the bytes, in rounds: an op that reads bytes this trip writes
+    // (or copies with a period other than 1/2/4/8) starts a new round, so a
+    // slot's round is the number of such ops at or before it.  In a round
+    // every source is read before any write; writes may spill up to 15
+    // bytes past an op's end, into later ops of the same or a later round
+    // (rewritten after) or past the trip's output (not made yet; in the ring,
+    // older than the 240-byte near window) -- see qo_put_round1.
     {
-      bool pend = (my_n > 0) & (my_kind != 2u);
-      bool done = !pend;
+      const bool mv = (my_n > 0) & !my_far;
+      const uint32_t depm = (uint32_t)(ballot(mv & my_dep) >> qs) & 0xfu;
+      const uint32_t rnd = (uint32_t)__builtin_popcount(depm & ((2u << g) - 1u));
+      const bool pat = (my_kind == 3u) & (my_dist <= 8) & ((my_dist & (my_dist - 1)) == 0);
+      const bool slow = (my_kind == 3u) & !pat;
 #pragma clang loop unroll(disable)
-      for (;;) {
-        const uint64_t dm = ballot(done);
-        const uint32_t qm = (uint32_t)(dm >> (lane & ~3u)) & 0xfu;
-        const uint32_t low = (1u << g) - 1u;
-        const bool ready = pend & (!my_dep | ((qm & low) == low));
-        if (ballot(ready) == 0) break;
-        u32x4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
-        if (ready) {
-          if (my_kind == 3u) {
-            // dist < n: the dist bytes before my_at repeat (snappy.c:329-330)
-            const uint32_t d = my_dist;
-            if ((d <= 8) & ((d & (d - 1)) == 0)) {
-              const u32x4 s0 = lrd16(ob + ((my_at - d) & (kOR - 1)));
-              const uint32_t b0 = s0.x & 0xffu, h0 = s0.x & 0xffffu;
-              const uint32_t px = d == 1 ? b0 * 0x01010101u : (d == 2 ? h0 | (h0 << 16) : s0.x);
-              const uint32_t py = d == 8 ? s0.y : px;
-              c0 = c1 = c2 = c3 = u32x4{px, py, px, py};
+      for (uint32_t r = 0; ballot(mv & (rnd >= r)); ++r) {
+        const bool on = mv & (rnd == r);
+        u32x4 c0, c1 = {0, 0, 0, 0}, c2 = c1, c3 = c1;
+        const uint8_t* sp = my_kind == 0u ? ib + (my_src & (kIR - 1)) : ob + (my_src & (kOR - 1));
+        // period 1/2/4/8 (snappy.c:329-330): the dist bytes before my_at repeat
+        const uint32_t d = my_dist;
+        const u32x4 s0 = lrd16(pat ? ob + ((my_at - d) & (kOR - 1)) : sp);
+        const uint32_t b0 = s0.x & 0xffu, h0 = s0.x & 0xffffu;
+        const uint32_t px = d == 1 ? b0 * 0x01010101u : (d == 2 ? h0 | (h0 << 16) : s0.x);
+        const uint32_t py = d == 8 ? s0.y : px;
+        c0 = pat ? u32x4{px, py, px, py} : s0;
+        if (ballot(on & !pat & (my_n > 16))) c1 = lrd16(sp + 16);
+        if (ballot(on & !pat & (my_n > 32))) c2 = lrd16(sp + 32);
+        if (ballot(on & !pat & (my_n > 48))) c3 = lrd16(sp + 48);
+        c1 = pat ? c0 : c1;
+        c2 = pat ? c0 : c2;
+        c3 = pat ? c0 : c3;
+        order();
+        qo_put_round1(ob, my_at, my_n, on & !slow, c0, c1, c2, c3, osink);
+        order();
+        if (ballot(on & slow)) {
+          // other periods (dist < n, not 1/2/4/8): byte by byte, the
+          // reference's forward loop (never in fillseq)
+          if (on & slow) {
+#pragma clang loop unroll(disable)
+            for (uint32_t b = 0; b < my_n; ++b) {
+              const uint8_t v = ob[(my_at + b - my_dist) & (kOR - 1)];
+              order();
+              const uint32_t rr = (my_at + b) & (kOR - 1);
+              ob[rr] = v;
+              if (rr < 64) ob[rr + kOR] = v;
+              order();
             }
-          } else {
-            const uint8_t* sp = my_kind == 0u ? ib + (my_src & (kIR - 1))
-                                              : ob + (my_src & (kOR - 1));
-            c0 = lrd16(sp);
-            if (my_n > 16) c1 = lrd16(sp + 16);
-            if (my_n > 32) c2 = lrd16(sp + 32);
-            if (my_n > 48) c3 = lrd16(sp + 48);
           }
+          order();
         }
-        order();
-        // other periods < 16 (never in fillseq): byte by byte below
-        const bool slow = ready & (my_kind == 3u) & !((my_dist <= 8) & ((my_dist & (my_dist - 1)) == 0));
-        if (ready & !slow) qo_put(ob, my_at, my_n, c0, c1, c2, c3, osink);
-        if (slow) {
-#pragma clang loop unroll(disable)
-          for (uint32_t b = 0; b < my_n; ++b) {
-            const uint8_t v = ob[(my_at + b - my_dist) & (kOR - 1)];
-            order();
-            const uint32_t r = (my_at + b) & (kOR - 1);
-            ob[r] = v;
-            if (r < 64) ob[r + kOR] = v;
-            order();
-          }
-        }
-        order();
-        done = done | ready;
-        pend = pend & !ready;
       }
     }
 
-    // ---- the far copy's bytes, 16 a lane, from the flushed output (they end
-    // before made0 - 176 < F): they land at the start of the next trip.
-    if (has_far) {
-      const uint32_t k0 = 16 * g;
-      if (k0 < flen) fv = ld16((gptr<const uint8_t>)(dst + far_src + k0));
-    }
-
-    // ---- refills: the next 64 stream bytes once the 64 they overwrite in the
-    // ring are consumed; up to two a trip.
+    // ---- refills: the next 64 stream bytes once the 64 they overwrite in
+    // the ring are consumed; up to two a trip, landed at the top of the next.
+    // (Issued at the top of the trip instead, from the trip's start
+    // position, they decoded C2 wrongly -- an unexplained failure, see
+    // DESIGN.md 4.2 -- and were slower: 312 against 305 us.)
     {
       const uint32_t cons = orem > 0 ? olp : pos;
-      const bool r0 = (st == 1) & (in_req < slen) & (in_req <= cons + 64);
-      if (r0) {
-        const uint32_t o = in_req + 16 * g;
-        if (o < slen) rv0 = ld16(src + o);
-        ra0 = o & (kIR - 1);
-        in_req += 64;
-      }
-      const bool r1 = r0 & (in_req < slen) & (in_req <= cons + 64);
-      if (r1) {
-        const uint32_t o = in_req + 16 * g;
-        if (o < slen) rv1 = ld16(src + o);
-        ra1 = o & (kIR - 1);
-        in_req += 64;
-      }
+      const bool q0 = (st == 1) & (in_req < slen) & (in_req <= cons + 64);
+      const uint32_t o0 = in_req + 16 * g;
+      if (q0 & (o0 < slen)) rv0 = ld16(src + o0);
+      ra0 = q0 ? ib + (o0 & (kIR - 1)) : isink;
+      rm0 = (q0 & ((o0 & (kIR - 1)) < 64)) ? ib + kIR + (o0 & (kIR - 1)) : isink;
+      in_req = q0 ? in_req + 64 : in_req;
+      const bool q1 = q0 & (in_req < slen) & (in_req <= cons + 64);
+      const uint32_t o1 = in_req + 16 * g;
+      if (q1 & (o1 < slen)) rv1 = ld16(src + o1);
+      ra1 = q1 ? ib + (o1 & (kIR - 1)) : isink;
+      rm1 = (q1 & ((o1 & (kIR - 1)) < 64)) ? ib + kIR + (o1 & (kIR - 1)) : isink;
+      in_req = q1 ? in_req + 64 : in_req;
     }
   }
 
