@@ -72,9 +72,9 @@ class Codec:
     # -- batches (pthreads, static round-robin partition: cpu_batch.c) --
 
     def _batch(self, mode: int, fn, threads, buf, off, ln, out, ooff, olen, status,
-               partition: int = 0):
+               partition: int = 0, reps: int = 1):
         drv = _driver()
-        rc = drv.cpu_batch_run2(mode, C.cast(fn, C.c_void_p), threads, partition,
+        rc = drv.cpu_batch_run3(mode, C.cast(fn, C.c_void_p), threads, partition, reps,
                                buf.ctypes.data, off.ctypes.data, ln.ctypes.data,
                                out.ctypes.data, ooff.ctypes.data,
                                olen.ctypes.data if olen is not None else None,
@@ -118,6 +118,9 @@ def _driver():
         d.cpu_batch_run2.restype = C.c_int
         d.cpu_batch_run2.argtypes = ([C.c_int, C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 7
                                      + [C.c_uint32])
+        d.cpu_batch_run3.restype = C.c_int
+        d.cpu_batch_run3.argtypes = ([C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_uint32]
+                                     + [C.c_void_p] * 7 + [C.c_uint32])
         _drv = d
     return _drv
 
@@ -434,7 +437,9 @@ def baseline_plan(codec: Codec, buf, off, ln, thread_counts, reps: int = 5,
     threads fault their own pages in, so on a multi-socket host each thread
     writes memory of its own NUMA node (buffers reused from a run with
     another partition would keep that run's placement), and the timed runs
-    reuse those pre-faulted pages.  Returns GiB/s per (threads, partition)
+    reuse those pre-faulted pages.  Each timed call makes enough passes over
+    the blocks (>= ~0.2 s) that starting the threads does not count.
+    Returns GiB/s per (threads, partition)
     plus the compressed output (for the byte-for-byte check against the
     GPU's)."""
     n = int(ln.shape[0])
@@ -455,15 +460,20 @@ def baseline_plan(codec: Codec, buf, off, ln, thread_counts, reps: int = 5,
             olen = np.zeros(n, dtype=np.uint32)
             st = np.zeros(n, dtype=np.uint8)
             te, td = [], []
+            ie = idd = 1               # passes per timed call (amortises thread start-up)
             for r in range(reps + 1):
                 t0 = time.perf_counter()
-                codec._batch(0, codec.f_encode, t, buf, off, ln, comp, ooff, olen, None, part)
+                codec._batch(0, codec.f_encode, t, buf, off, ln, comp, ooff, olen, None, part, ie)
                 t1 = time.perf_counter()
-                codec._batch(1, codec.f_decode, t, comp, ooff, olen, dec, doff, None, st, part)
+                codec._batch(1, codec.f_decode, t, comp, ooff, olen, dec, doff, None, st, part,
+                             idd)
                 t2 = time.perf_counter()
                 if r:                      # run 0 is the warm-up
-                    te.append(t1 - t0)
-                    td.append(t2 - t1)
+                    te.append((t1 - t0) / ie)
+                    td.append((t2 - t1) / idd)
+                else:                      # size the timed calls to >= ~0.2 s each
+                    ie = max(1, min(64, int(0.2 / max(t1 - t0, 1e-6)) + 1))
+                    idd = max(1, min(64, int(0.2 / max(t2 - t1, 1e-6)) + 1))
             if not bool((st == 1).all()):
                 raise RuntimeError("CPU baseline: reference decode rejected its own output")
             e, d = float(np.median(te)), float(np.median(td))

@@ -14,6 +14,12 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+int cpu_batch_run2(int mode, void *fn, int threads, int partition,
+                   const uint8_t *in, const uint64_t *in_off,
+                   const uint32_t *in_len, uint8_t *out,
+                   const uint64_t *out_off, uint32_t *out_len,
+                   uint8_t *status, uint32_t n);
+
 typedef size_t (*cb_encode_fn)(uint8_t *, const uint8_t *, size_t);
 typedef int (*cb_decode_fn)(uint8_t *, const uint8_t *, size_t);
 
@@ -31,13 +37,15 @@ typedef struct {
   uint32_t n;               /* blocks [first, n) with this stride */
   uint32_t stride;
   uint32_t first;
+  uint32_t reps;            /* passes over the partition (timing: amortises thread start) */
 } cb_job;
 
 static void *
 cb_worker(void *arg) {
   const cb_job *j = (const cb_job *)arg;
-  uint32_t i;
+  uint32_t i, r;
 
+  for (r = 0; r < j->reps; r++)
   for (i = j->first; i < j->n; i += j->stride) {
     const uint8_t *src = j->in + j->in_off[i];
     uint8_t *dst = j->out + j->out_off[i];
@@ -60,7 +68,7 @@ cb_worker(void *arg) {
  * caller passes untouched buffers).  Returns 0 on success, -1 if a thread
  * could not be started. */
 int
-cpu_batch_run2(int mode, void *fn, int threads, int partition,
+cpu_batch_run3(int mode, void *fn, int threads, int partition, uint32_t reps,
                const uint8_t *in, const uint64_t *in_off,
                const uint32_t *in_len, uint8_t *out,
                const uint64_t *out_off, uint32_t *out_len,
@@ -93,6 +101,7 @@ cpu_batch_run2(int mode, void *fn, int threads, int partition,
     j->out_off = out_off;
     j->out_len = out_len;
     j->status = status;
+    j->reps = reps < 1 ? 1 : reps;
     if (partition == 1) {
       j->first = (uint32_t)((uint64_t)n * (uint64_t)t / (uint64_t)threads);
       j->n = (uint32_t)((uint64_t)n * (uint64_t)(t + 1) / (uint64_t)threads);
@@ -132,4 +141,14 @@ cpu_batch_run(int mode, void *fn, int threads,
               uint8_t *status, uint32_t n) {
   return cpu_batch_run2(mode, fn, threads, 0, in, in_off, in_len, out, out_off,
                         out_len, status, n);
+}
+
+int
+cpu_batch_run2(int mode, void *fn, int threads, int partition,
+               const uint8_t *in, const uint64_t *in_off,
+               const uint32_t *in_len, uint8_t *out,
+               const uint64_t *out_off, uint32_t *out_len,
+               uint8_t *status, uint32_t n) {
+  return cpu_batch_run3(mode, fn, threads, partition, 1, in, in_off, in_len, out,
+                        out_off, out_len, status, n);
 }
