@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "builder.h"
 #include "dbformat.h"
@@ -56,6 +57,7 @@ main(int argc, char **argv) {
   ldb_bloom_t user_bloom, ifp;
   size_t pos = 0;
   int rc;
+  struct timespec ts0, ts1, ts2;
 
   if (argc < 3) {
     fprintf(stderr, "usage: %s DIR NUM_ENTRIES [BLOCK_SIZE [BLOOM_BITS]]\n", argv[0]);
@@ -87,6 +89,7 @@ main(int argc, char **argv) {
     ldb_buffer_concat(&ring, &piece);
   }
 
+  clock_gettime(CLOCK_MONOTONIC, &ts0);
   mem = ldb_memtable_create(&icmp);
   ldb_memtable_ref(mem);
 
@@ -110,12 +113,17 @@ main(int argc, char **argv) {
   ldb_filemeta_init(&meta);
   meta.number = 1;
 
+  clock_gettime(CLOCK_MONOTONIC, &ts1);
   iter = ldb_memiter_create(mem);
   rc = ldb_build_table(dir, &options, tables, iter, &meta);
   ldb_iter_destroy(iter);
+  clock_gettime(CLOCK_MONOTONIC, &ts2);
 
-  printf("rc=%d (%s) file_size=%lu\n", rc, ldb_strerror(rc),
-         (unsigned long)meta.file_size);
+  /* fill_s: memtable inserts; build_s: ldb_build_table (write, sync, reopen) */
+  printf("rc=%d (%s) file_size=%lu fill_s=%.3f build_s=%.3f\n", rc, ldb_strerror(rc),
+         (unsigned long)meta.file_size,
+         (ts1.tv_sec - ts0.tv_sec) + (ts1.tv_nsec - ts0.tv_nsec) * 1e-9,
+         (ts2.tv_sec - ts1.tv_sec) + (ts2.tv_nsec - ts1.tv_nsec) * 1e-9);
 
   ldb_tables_destroy(tables);
   ldb_memtable_unref(mem);

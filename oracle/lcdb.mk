@@ -11,7 +11,9 @@
 # Programs: lcdb's unchanged test suites that reach the codec (test/t-*.c)
 # and our harnesses: harness/build_table.c (config 5) and harness/
 # dump_blocks.c (every block of an .ldb as ldb_read_block returns it, the
-# pin of the block-framing rows).  Outputs only in _ref/.
+# pin of the block-framing rows), and harness/build_table_batched.c (config 5
+# through the batched lgs_table_* entry points; linked only as .gpu).
+# Outputs only in _ref/.
 #   make -C oracle -f lcdb.mk        (needs $(REF); the binaries travel)
 
 REF    ?= /root/reference
@@ -33,7 +35,7 @@ LIBSRC := $(addprefix src/util/,arena array atomic bloom buffer cache comparator
 TESTS  := snappy table db corruption simple recovery
 LIBOBJ := $(patsubst %,$(OUT)/obj/%.o,$(subst /,__,$(LIBSRC)))
 PROGS  := $(addprefix t-,$(TESTS)) build_table dump_blocks
-BINS   := $(foreach p,$(PROGS),$(OUT)/$(p).cpu $(OUT)/$(p).gpu)
+BINS   := $(foreach p,$(PROGS),$(OUT)/$(p).cpu $(OUT)/$(p).gpu) $(OUT)/build_table_batched.gpu
 
 ifneq ($(wildcard $(REF)/src/util/snappy.c),)
 all: $(BINS) $(OUT)/libref_bloom.so
@@ -57,6 +59,9 @@ $(OUT)/build_table.o: $(HERE)harness/build_table.c
 
 $(OUT)/dump_blocks.o: $(HERE)harness/dump_blocks.c
 	$(CC) $(CFLAGS) -c $< -o $@
+
+$(OUT)/build_table_batched.o: $(HERE)harness/build_table_batched.c $(HERE)../include/lcdb_gpu_snappy.h
+	$(CC) $(CFLAGS) -I$(HERE)../include -c $< -o $@
 
 # The reference's bloom filter behind a ctypes-callable shim (bloom row pin).
 $(OUT)/libref_bloom.so: $(HERE)harness/bloom_ref.c $(OUT)/liblcdb_core.a

@@ -101,3 +101,18 @@ def test_host_side_bloom_and_filter_block_sizes_match_oracle():
         nkeys = sum(len(b) for b in blocks)
         assert len(fb) <= bloom.filter_block_bound(nkeys, len(blocks), end, bpk)
         assert bloom.filter_block_scratch(end) > 0
+
+
+def test_integration_recipe_names_the_built_sources():
+    """INTEGRATION.md §1's hand-written hipcc line compiles exactly the
+    sources build.py compiles, with the export map, and every one exists."""
+    import re
+
+    from lcdb_amd import build
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = text[text.index("## 1. Build the library"):text.index("## 2.")]
+    named = re.findall(r"lcdb_amd/csrc/(\w+\.(?:cpp|hip))", block)
+    assert sorted(named) == sorted(build.HIP_SOURCES)
+    assert "--version-script=lcdb_amd/csrc/exports.map" in block
+    for s in named:
+        assert os.path.exists(os.path.join(ROOT, "lcdb_amd", "csrc", s))
