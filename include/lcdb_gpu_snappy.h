@@ -307,8 +307,12 @@ int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
 
 /* Process-wide kernel choices (A/B and tests; the defaults pick by batch):
      "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
+                | "quad" (four lanes per block; A/B only)
+     "wide":    "walk" (default) | "trips"  (decoder of outputs over 16 KiB:
+                the one-tag walk, or up to 8 tags per step; A/B only)
      "split":   "1" | "0"  (size-class split of mixed batches, see above)
-   Initial values: LGS_DECODE_KERNEL, LGS_NO_SPLIT=1, read once at load.
+   Initial values: LGS_DECODE_KERNEL, LGS_WIDE_DECODER, LGS_NO_SPLIT=1, read
+   once at load.
    LGS_EINVAL for an unknown name or value. */
 int lgs_set_option(const char *name, const char *value);
 

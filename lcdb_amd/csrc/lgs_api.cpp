@@ -730,6 +730,8 @@ Options& options_init() {
     if (dk && !strcmp(dk, "quad")) v->decoder = kDecQuad;
     const char* ns = getenv("LGS_NO_SPLIT");
     if (ns && *ns && strcmp(ns, "0")) v->split = 0;
+    const char* wd = getenv("LGS_WIDE_DECODER");
+    if (wd && !strcmp(wd, "trips")) v->wide = kWideTrips;
     return v;
   }();
   return *o;
@@ -811,6 +813,12 @@ int lgs_set_option(const char* name, const char* value) {
     if (!*value || *end || v < 0 || v > 1000000)
       return fail(LGS_EINVAL, "inject_alloc_failures '%s' (0..1000000)", value);
     g_inject_alloc_failures = (int)v;
+    return LGS_OK;
+  }
+  if (!strcmp(name, "wide")) {
+    if (!strcmp(value, "walk") || !*value) o.wide = kWideWalk;
+    else if (!strcmp(value, "trips")) o.wide = kWideTrips;
+    else return fail(LGS_EINVAL, "wide '%s' (walk or trips)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "split")) {

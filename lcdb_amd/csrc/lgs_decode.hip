@@ -472,6 +472,11 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   }
 }
 
+// LDS byte address of a __shared__ pointer (for inline-asm ds_* operands).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+
 // One byte of global memory through an agent-scope load (not served from a
 // possibly stale L1 line): the wide decoder's reads of output it flushed.
 __device__ __forceinline__ uint8_t gl_byte(const uint8_t* p) {
@@ -760,6 +765,346 @@ __global__ __launch_bounds__(64) void decode_wide_kernel(
     } while (apos < wend);
   }
   sb[pend] = (uint8_t)pv;
+  order();
+  if (st == 1 && made != want) st = 0;                        // snappy.c:337
+  if (st == 1) flush(want);
+  if (lane == 0) {
+    status[i] = (uint8_t)st;
+    out_len[i] = st == 1 ? want : 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Trip decoder (round 3): decode_wide_kernel's rings, staging and flushes,
+// but the walk moves up to G = 8 tags per step ("trip") instead of one.
+// C3's fillseq 64 KiB class decoded at ~130 GiB/s in the wide decoder: 1 024
+// blocks are 1 024 serial walks, one per SIMD, and each tag cost ~380 cycles
+// of one wave's dependent instructions and LDS round trips (3 072 tags per
+// block).  A trip:
+//   * chain (scalar): from apos, follow the window's parsed tags while each
+//     passes its one range test (the same test as the wide walk: a common tag
+//     whose snappy.c:263 / :323 bounds hold at its own output offset), up to
+//     G tags and the window's end; op k's window lane and output offset go to
+//     lane group k (lanes 8k .. 8k+7);
+//   * moves (lane groups): op k's bytes i = j, j+8, .. (j = lane & 7), one
+//     byte per LDS access, ring-masked, so the writes are exact and never
+//     touch a neighbour's bytes;
+//   * rounds: a copy whose source reaches into this trip's output (dependent)
+//     must read after the ops it depends on have written.  Op k runs in round
+//     r_k = the number of dependent ops among 0..k; every round reads, then
+//     writes (one wave's LDS accesses execute in issue order).  r_k is larger
+//     than every earlier op's round exactly when op k is dependent.
+// A tag that fails the test (long literal, overlapping, COPY4 or far copy,
+// or a bound) ends the chain; if it is the trip's first, the exact scalar step
+// of the wide walk decodes it alone.  By simulation on fillseq 64 KiB blocks
+// (G = 8, 64-byte windows): 5.7 tags per trip, 2.0 rounds per trip.
+// Measured (profiles/r3s_wide_trips_ab.txt): exact, but C3's fillseq 64 KiB
+// class decodes at 80 GiB/s against the walk's 129.  A lone wave per SIMD
+// runs ~10 cycles per instruction; the walk spends ~28 instructions per tag,
+// a trip ~340 for 5.7 tags (the scalar chain alone ~25 per tag).  Not the
+// default; lgs_set_option("wide", "trips") selects it.
+// ---------------------------------------------------------------------------
+template <uint32_t OUT, uint32_t IN>
+__global__ __launch_bounds__(64) void decode_trips_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count) {
+  constexpr uint32_t kG = 8;                 // ops per trip (8 lanes each)
+  constexpr uint32_t kOut = OUT;             // output ring
+  constexpr uint32_t kIn = IN;               // input ring
+  constexpr uint32_t kMirror = 80;           // stream bytes kIn.. mirror ring offsets 0..79
+  constexpr uint32_t kSink = kOut + kIn + kMirror;   // a dword per lane for unused writes
+  constexpr uint32_t kBuf = kSink + 4 * kWave;
+  constexpr uint32_t kRefill = kIn / 2;
+  constexpr uint32_t kGran = kRefill / 1024;
+  constexpr uint32_t kFlushAt = kOut / 4;
+  constexpr uint32_t kFar = kOut - kWave;
+  static_assert(kFlushAt + 4224 <= kOut && (kGran == 1 || kGran == 2), "ring sizes");
+  __shared__ __attribute__((aligned(16))) uint8_t sb[kBuf];
+  uint8_t* const ib = sb + kOut;
+
+  const uint32_t slot = blockIdx.x;
+  if (slot >= (count ? uni(*count) : n)) return;
+  const uint32_t i = uni(index ? index[slot] : slot);
+  const uint32_t lane = lane_id();
+  const uint32_t grp = lane >> 3, sub = lane & 7u;
+  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
+  const uint32_t slen = uni(in_len[i]);
+  const uint64_t doff = uni64(out_off[i]);
+  const gptr<uint8_t> dst = to_global(out) + doff;
+  const uint8_t* const dgen = out + doff;
+  const uint32_t cap = uni(out_cap[i]);
+  const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+  const gptr<uint8_t> dal = dst - oshift;
+
+  uint32_t st = 1, want = 0, hlen = 0;
+  {
+    const uint64_t h = uni64(view8(src));
+    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
+      const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
+      if ((b & 0x80u) == 0) {
+        want |= b << (7 * k);
+        hlen = k + 1;
+        break;
+      }
+      want |= (b & 0x7fu) << (7 * k);
+    }
+    if (hlen == 0 || want > 0x7fffffffu) st = 0;              // snappy.c:405-409
+    else if (want > cap) st = 2;
+  }
+
+  uint32_t staged = 0;
+  u32x4 pf0 = {0, 0, 0, 0}, pf1 = pf0;
+  auto prefetch = [&]() {
+    const uint32_t c0 = staged + 16 * lane, c1 = c0 + 1024;
+    if (c0 < slen) pf0 = ld16(src + c0);
+    if (kGran == 2 && c1 < slen) pf1 = ld16(src + c1);
+  };
+  auto land = [&]() {
+    __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
+    const uint32_t r0 = (staged + 16 * lane) & (kIn - 1), r1 = (r0 + 1024) & (kIn - 1);
+    *reinterpret_cast<u32x4*>(ib + r0) = pf0;
+    if (r0 < kMirror) *reinterpret_cast<u32x4*>(ib + kIn + r0) = pf0;
+    if (kGran == 2) {
+      *reinterpret_cast<u32x4*>(ib + r1) = pf1;
+      if (r1 < kMirror) *reinterpret_cast<u32x4*>(ib + kIn + r1) = pf1;
+    }
+    order();
+    staged += kRefill;
+    prefetch();
+  };
+
+  uint32_t made = 0, F = 0;
+  auto flush = [&](uint32_t to) {
+    const uint32_t g0 = (F + oshift) >> 4, g1 = (to + oshift + 15) >> 4;
+    for (uint32_t g = g0 + lane; g < g1; g += kWave) {
+      const uint32_t lo = 16 * g, hi = lo + 16;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(sb + (lo & (kOut - 1)));
+      if (lo >= F + oshift && hi <= to + oshift) {
+        *(gptr<u32x4>)(dal + lo) = v;
+      } else {
+        for (uint32_t b = lo; b < hi; ++b)
+          if (b >= F + oshift && b < to + oshift) dal[b] = (uint8_t)byte_of(v, b - lo);
+      }
+    }
+    F = to;
+  };
+
+  uint32_t apos = hlen;
+  const uint32_t aend = slen;
+  if (st == 1) {
+    prefetch();
+    land();
+    land();
+  }
+  while (st == 1 && apos < aend) {                            // snappy.c:208
+    const uint32_t w = apos;
+    const uint32_t wend = aend - w < kWave ? aend : w + kWave;
+    while (staged < aend && staged <= w + kRefill) land();
+    if (made - F >= kFlushAt) flush(((made + oshift) & ~15u) - oshift);
+    uint32_t flo, frng, fsrc, fpk;
+    {
+      const uint32_t q = w + lane;
+      const uint32_t t = lds_ld32(ib, q & (kIn - 1));
+      const uint32_t tag = t & 0xffu, kind = tag & 3u, m0 = tag >> 2;
+      const bool lit = kind == 0;
+      const uint32_t len = kind == 1 ? 4 + (m0 & 7u) : m0 + 1;     // snappy.c:216, 276, 289
+      const uint32_t dist = kind == 1 ? ((tag & 0xe0u) << 3) | ((t >> 8) & 0xffu)
+                                      : (t >> 8) & 0xffffu;          // snappy.c:279, 292
+      const uint32_t step = lit ? len + 1 : kind + 1;
+      const int32_t hi = (int32_t)want - (int32_t)len;
+      const uint32_t lo = lit ? 0u : dist;
+      const bool common = (lit ? m0 < 60 : (kind != 3) & (dist >= len) & (dist != 0) &
+                                           (dist <= kFar)) & (step <= aend - q);
+      const bool fast = common & (hi >= (int32_t)lo);
+      flo = fast ? lo : 0xffffffffu;
+      frng = fast ? (uint32_t)(hi - (int32_t)lo) : 0u;
+      // A literal's first stream position; a copy's source less its output offset.
+      fsrc = lit ? q + 1 : 0u - dist;
+      fpk = len | (step << 8) | (lit ? 0u : 0x10000u);
+    }
+    do {
+      // ---- chain: up to kG tags from apos, each passing its range test.
+      uint32_t nops = 0, m = made, maxlen = 0;
+      uint32_t my_d = 0, my_m = 0;
+      while (nops < kG && apos < wend) {
+        const uint32_t d = apos - w;
+        const uint32_t rlo = __builtin_amdgcn_readlane(flo, d);
+        const uint32_t rrng = __builtin_amdgcn_readlane(frng, d);
+        if (m - rlo > rrng) break;
+        const uint32_t pk = __builtin_amdgcn_readlane(fpk, d);
+        if (grp == nops) {
+          my_d = d;
+          my_m = m;
+        }
+        const uint32_t ln = pk & 0xffu;
+        maxlen = ln > maxlen ? ln : maxlen;
+        m += ln;
+        apos += (pk >> 8) & 0xffu;
+        ++nops;
+      }
+      if (nops > 0) {
+        // ---- the trip's moves, in rounds.
+        const bool act = grp < nops;
+        const uint32_t opk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(my_d << 2), (int)fpk);
+        const uint32_t os = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(my_d << 2), (int)fsrc);
+        const uint32_t L = act ? (opk & 0xffu) : 0u;
+        const bool lit = (opk >> 16) == 0;
+        const uint32_t s0 = lit ? os : my_m + os + oshift;     // ring coordinate of byte 0
+        const uint32_t smask = lit ? kIn - 1 : kOut - 1;
+        const uint32_t sbase = lit ? kOut : 0u;
+        const uint32_t d0 = my_m + oshift;
+        const bool dep = act & !lit & (my_m + os + L > made);   // source reaches into this trip
+        const uint64_t db = ballot(dep);
+        const uint64_t upto = grp == 7 ? ~0ull : ((1ull << (8 * grp + 8)) - 1ull);
+        const uint32_t rnd = (uint32_t)__builtin_popcountll(db & upto) >> 3;
+        const uint32_t nr = ((uint32_t)__builtin_popcountll(db) >> 3) + 1;
+        const uint32_t T = (maxlen + 7) >> 3;
+        // Byte slot t of this lane: op byte sub + 8t.  Reads are harmless
+        // anywhere in the rings (ring-masked), so only writes are steered:
+        // bytes outside this round's ops go to the lane's own sink dword.
+        uint32_t ra[8], wa[8];
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t) {
+          ra[t] = sbase + ((s0 + sub + 8 * t) & smask);
+          wa[t] = (d0 + sub + 8 * t) & (kOut - 1);
+        }
+        const uint32_t sink = kSink + 4 * lane;
+        const uint32_t lb = lds_addr(sb);
+        for (uint32_t r = 0; r < nr; ++r) {
+          const bool go = rnd == r;
+          // Reads of slots 0-3 always, 4-7 when an op is longer than 32
+          // bytes; one wait; then the writes.  (Written as C++ with per-slot
+          // conditions, hipcc put an lgkmcnt(0) before every read.)
+          uint32_t v0, v1, v2, v3, v4 = 0, v5 = 0, v6 = 0, v7 = 0;
+          asm volatile(
+              "ds_read_u8 %0, %4\n\tds_read_u8 %1, %5\n\t"
+              "ds_read_u8 %2, %6\n\tds_read_u8 %3, %7"
+              : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+              : "v"(lb + ra[0]), "v"(lb + ra[1]), "v"(lb + ra[2]), "v"(lb + ra[3])
+              : "memory");
+          if (T > 4)
+            asm volatile(
+                "ds_read_u8 %0, %4\n\tds_read_u8 %1, %5\n\t"
+                "ds_read_u8 %2, %6\n\tds_read_u8 %3, %7"
+                : "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7)
+                : "v"(lb + ra[4]), "v"(lb + ra[5]), "v"(lb + ra[6]), "v"(lb + ra[7])
+                : "memory");
+          uint32_t w[8];
+#pragma unroll
+          for (uint32_t t = 0; t < 8; ++t) w[t] = lb + ((go & (sub + 8 * t < L)) ? wa[t] : sink);
+          asm volatile(
+              "s_waitcnt lgkmcnt(0)\n\t"
+              "ds_write_b8 %0, %4\n\tds_write_b8 %1, %5\n\t"
+              "ds_write_b8 %2, %6\n\tds_write_b8 %3, %7"
+              :
+              : "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(v0), "v"(v1), "v"(v2), "v"(v3)
+              : "memory");
+          if (T > 4)
+            asm volatile(
+                "ds_write_b8 %0, %4\n\tds_write_b8 %1, %5\n\t"
+                "ds_write_b8 %2, %6\n\tds_write_b8 %3, %7"
+                :
+                : "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]), "v"(v4), "v"(v5), "v"(v6), "v"(v7)
+                : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        made = m;
+        continue;
+      }
+      // ---- the exact tag step of snappy.c:210-324 for one tag.
+      const uint64_t tv = uni64(lds_ld64(ib, apos & (kIn - 1)));
+      const uint32_t tg = (uint32_t)tv & 0xffu, kd = tg & 3u;
+      const uint32_t hi = (uint32_t)(tv >> 8), left = aend - apos;
+      bool bad = false;
+      uint32_t x = 0, ds = 0, nb = 0, adv = 0;
+      if (kd == 0) {                                // literal, snappy.c:210-273
+        uint32_t mm = tg >> 2, hl = 1;
+        if (mm >= 60) {
+          const uint32_t extra = mm - 59;
+          bad = left - 1 < extra;
+          mm = extra == 4 ? hi : (hi & ((1u << (8 * (extra & 3u))) - 1u));
+          hl += extra;
+        }
+        nb = mm + 1;
+        bad = bad || mm >= 0x7fffffffu || nb > left - hl || nb > want - made;   // :258, :263
+        x = apos + hl;
+        adv = hl + nb;
+      } else {                                      // copies, snappy.c:276-324
+        const uint32_t chl = kd == 1 ? 2u : (kd == 2 ? 3u : 5u);
+        nb = kd == 1 ? 4 + ((tg >> 2) & 7u) : 1 + (tg >> 2);
+        ds = kd == 1 ? ((tg & 0xe0u) << 3) | (hi & 0xffu) : (kd == 2 ? hi & 0xffffu : hi);
+        bad = left < chl || ds == 0 || ds >= 0x80000000u || made < ds || nb > want - made;
+        adv = chl;
+      }
+      if (bad) {
+        st = 0;
+        break;
+      }
+      const uint32_t u0 = made + oshift;
+      if (kd == 0 && nb <= kWave) {
+        uint32_t v = 0;
+        if (lane < nb) v = ib[(x + lane) & (kIn - 1)];
+        order();
+        if (lane < nb) sb[(u0 + lane) & (kOut - 1)] = (uint8_t)v;
+        order();
+      } else if (kd == 0) {
+        // A long literal, as in decode_wide_kernel.
+        const uint32_t head0 = (16u - (u0 & 15u)) & 15u;
+        const uint32_t head = head0 < nb ? head0 : nb;
+        const uint32_t body = (nb - head) & ~15u;
+        const gptr<const uint8_t> ls = src + x;
+        if (lane < head) sb[(u0 + lane) & (kOut - 1)] = ls[lane];
+        order();
+        for (uint32_t j = head; j < head + body; j += 4096) {
+          if (made + j - F >= kFlushAt) flush(((made + j + oshift) & ~15u) - oshift);
+          u32x4 v[4];
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t jj = j + 16 * (lane + 64 * k);
+            if (jj < head + body) v[k] = ld16(ls + jj);
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t jj = j + 16 * (lane + 64 * k);
+            if (jj < head + body)
+              *reinterpret_cast<u32x4*>(sb + ((u0 + jj) & (kOut - 1))) = v[k];
+          }
+          order();
+        }
+        if (made + nb - F >= kFlushAt) flush(((made + head + body + oshift) & ~15u) - oshift);
+        {
+          const uint32_t jj = head + body + lane;
+          if (jj < nb) sb[(u0 + jj) & (kOut - 1)] = ls[jj];
+        }
+        order();
+        if (x + nb > staged) {
+          __builtin_amdgcn_s_waitcnt(0x0f70);
+          staged = (x + nb) & ~15u;
+          prefetch();
+        }
+      } else if (ds > kFar) {
+        // Beyond the ring: the flushed output, once its stores have drained.
+        __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
+        uint8_t v = 0;
+        if (lane < nb) v = gl_byte(dgen + made - ds + lane);
+        if (lane < nb) sb[(u0 + lane) & (kOut - 1)] = v;
+        order();
+      } else {
+        // dist < len repeats the dist-byte pattern (snappy.c:329-330).
+        uint32_t v = 0;
+        if (lane < nb) v = sb[(u0 - ds + (ds >= nb ? lane : lane % ds)) & (kOut - 1)];
+        order();
+        if (lane < nb) sb[(u0 + lane) & (kOut - 1)] = (uint8_t)v;
+        order();
+      }
+      made += nb;
+      apos += adv;
+    } while (apos < wend);
+  }
   order();
   if (st == 1 && made != want) st = 0;                        // snappy.c:337
   if (st == 1) flush(want);
@@ -1753,6 +2098,19 @@ static hipError_t launch_decode_wide(const DecodeArgs& a, hipStream_t s) {
                      a.count);
   return hipGetLastError();
 }
+template <uint32_t OUT, uint32_t IN>
+static hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((decode_trips_kernel<OUT, IN>), dim3(a.n), dim3(64), 0, s, a.in, a.in_off,
+                     a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n,
+                     a.count);
+  return hipGetLastError();
+}
+// The wide class: the one-tag walk unless the "wide" option says "trips".
+static hipError_t launch_decode_big(const DecodeArgs& a, hipStream_t s) {
+  if (options().wide.load(std::memory_order_relaxed) == kWideTrips)
+    return launch_decode_trips<32768, 4096>(a, s);
+  return launch_decode_wide<32768, 4096>(a, s);
+}
 // The 16 KiB class stays in decode_kernel's in-place image (18 KB, eight
 // waves per CU): the rings at 8 KiB + 2 KiB (10.4 KB, fourteen waves) were
 // slower on C3's 16 KiB classes (fillseq 212 -> 204 GiB/s, random 838 -> 690).
@@ -1775,11 +2133,11 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
   LGS_TRY(launch_decode_mid(c, s));
   if (max_out > kDecCap1) {            // (classes above max_out are empty)
     c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
-    LGS_TRY((launch_decode_wide<32768, 4096>(c, s)));
+    LGS_TRY(launch_decode_big(c, s));
   }
   if (max_out > kDecCap2) {
     c.index = list + 3 * (size_t)a.n; c.count = cnt + 3;
-    LGS_TRY((launch_decode_wide<32768, 4096>(c, s)));
+    LGS_TRY(launch_decode_big(c, s));
   }
   return scratch.release();
 }
@@ -1795,7 +2153,7 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
     return launch_decode_ring(a, s);
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_mid(a, s);
-  return launch_decode_wide<32768, 4096>(a, s);
+  return launch_decode_big(a, s);
 }
 
 }  // namespace lgs

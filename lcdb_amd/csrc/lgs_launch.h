@@ -15,9 +15,13 @@ namespace lgs {
 // LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
 // launch path reads the environment).
 enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3 };
+// Outputs over the 16 KiB class: the one-tag walk (default) or the trip
+// decoder (up to 8 tags per step; exact, slower: DESIGN §4.2).
+enum WideKernel { kWideWalk = 0, kWideTrips = 1 };
 struct Options {
   std::atomic<int> decoder{kDecAuto};   // DecodeKernel
   std::atomic<int> split{1};            // size-class split of mixed batches
+  std::atomic<int> wide{0};             // WideKernel: the decoder of the wide class
 };
 Options& options();
 

@@ -30,8 +30,10 @@
  * through a memtable: the memtable iterates them in this same order.
  *
  * usage: build_table_batched DIR NUM_ENTRIES [BLOCK_SIZE]
- * prints: rc=0 file_size=N blocks=N cut_s=.. write_s=.. finish_s=.. io_s=..
- *         read_s=.. raw_bytes=N
+ * prints: rc=0 file_size=N blocks=N raw_bytes=N cut_s=.. init_s=.. write_s=..
+ *         write_warm_s=.. finish_s=.. io_s=.. read_s=.. read_bad=0
+ * (init_s: HIP start-up; write_s: the first write call, which also grows the
+ * pinned staging arena; write_warm_s: the same call again.)
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -131,7 +133,8 @@ main(int argc, char **argv) {
   uint64_t end = 0, at;
   size_t pos = 0;
   int pending = 0, rc;
-  double t0, t1, t2, t3, t4, t5;
+  double t0, t1, ti, t2, t2w, t3, t4, t5;
+  uint64_t end_warm = 0;
   FILE *f;
 
   if (argc < 3) {
@@ -223,6 +226,12 @@ main(int argc, char **argv) {
     return 4;
   keys_off[nb] = keys_at;
   t1 = now();
+  /* HIP runtime and device start-up, timed apart from the codec. */
+  if (lgs_device_count() <= 0) {
+    fprintf(stderr, "no device\n");
+    return 5;
+  }
+  ti = now();
 
   /* 2. Every data block in one call: compress, 12.5 % rule, trailers, packing. */
   hoff = xrealloc(NULL, nb * sizeof(*hoff));
@@ -236,6 +245,16 @@ main(int argc, char **argv) {
     return 5;
   }
   t2 = now();
+  /* The same call again: the first one also grew the library's pinned
+     staging arena to this table's size; the second is the steady state a
+     bulk writer sees from its second table on. */
+  rc = lgs_table_write_host(raw, raw_off, raw_len, nb, LGS_SNAPPY_COMPRESSION, 0, file, file_cap,
+                            hoff, hsize, &end_warm);
+  if (rc != LGS_OK || end_warm != end) {
+    fprintf(stderr, "lgs_table_write_host (warm): %d (%s)\n", rc, lgs_last_error());
+    return 5;
+  }
+  t2w = now();
 
   /* 3. Metaindex, index, footer (table_builder.c:266-363; no filter policy). */
   at = end;
@@ -298,10 +317,10 @@ main(int argc, char **argv) {
       bad++;
   }
 
-  printf("rc=%d file_size=%lu blocks=%u raw_bytes=%lu cut_s=%.3f write_s=%.3f finish_s=%.3f "
-         "io_s=%.3f read_s=%.3f read_bad=%u\n",
-         bad ? 1 : 0, (unsigned long)at, nb, (unsigned long)raw_at, t1 - t0, t2 - t1, t3 - t2,
-         t4 - t3, t5 - t4, bad);
+  printf("rc=%d file_size=%lu blocks=%u raw_bytes=%lu cut_s=%.3f init_s=%.3f write_s=%.3f "
+         "write_warm_s=%.3f finish_s=%.3f io_s=%.3f read_s=%.3f read_bad=%u\n",
+         bad ? 1 : 0, (unsigned long)at, nb, (unsigned long)raw_at, t1 - t0, ti - t1, t2 - ti,
+         t2w - t2, t3 - t2w, t4 - t3, t5 - t4, bad);
 
   ldb_blockgen_clear(&data);
   ldb_buffer_clear(&last_key);

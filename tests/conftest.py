@@ -70,4 +70,4 @@ def force():
 
     yield set_
     for name in touched:
-        _native.set_option(name, {"decoder": "auto", "split": "1"}[name])
+        _native.set_option(name, {"decoder": "auto", "split": "1", "wide": "walk"}[name])

@@ -439,9 +439,12 @@ def _copy2(length: int, dist: int) -> bytes:
     return bytes([((length - 1) << 2) | 2, dist & 255, dist >> 8])
 
 
-def test_decode_wide_far_copies_long_literals_and_rejects(gpu):
-    # Outputs over the 16 KiB class go to the wide decoder (a 32 KiB output
-    # ring flushed to HBM, a 4 KiB stream ring refilled 2 KiB at a time).
+@pytest.mark.parametrize("wide", ["trips", "walk"])
+def test_decode_wide_far_copies_long_literals_and_rejects(gpu, force, wide):
+    # Outputs over the 16 KiB class go to the wide decoders (a 32 KiB output
+    # ring flushed to HBM, a 4 KiB stream ring refilled 2 KiB at a time; the
+    # trip decoder moves up to 8 tags a step, the walk one).
+    force("wide", wide)
     # Hand-made streams put copies beyond the ring (dist > 32 704, read back
     # from HBM), literals across many refills and flushes, and every kind of
     # reject at different depths; real 64 KiB / 100 KB / 300 KB blocks and
@@ -510,3 +513,81 @@ def test_decode_wide_far_copies_long_literals_and_rejects(gpu):
             assert code == gpu.LGS_ST_OK and o == exp, k
             oks += 1
     assert oks >= 13
+
+
+def _trip_stress_stream(rng, want: int) -> bytes:
+    """Short literals and COPY1/COPY2s with small distances: many copies whose
+    source is the output of the same trip (chains of dependent copies), some
+    overlapping (dist < len) and some COPY4s, for the trip decoder's rounds."""
+    out = bytearray()
+    s = bytearray()
+    while len(out) < want:
+        r = rng.random()
+        room = want - len(out)
+        if len(out) < 8 or r < 0.35:
+            n = min(rng.randrange(1, 61), room)
+            b = bytes(rng.randrange(256) for _ in range(n))
+            s += bytes([(n - 1) << 2]) + b
+            out += b
+            continue
+        n = min(rng.randrange(4, 65), room)
+        if n < 4:
+            b = bytes(rng.randrange(256) for _ in range(n))
+            s += bytes([(n - 1) << 2]) + b
+            out += b
+            continue
+        if r < 0.45:
+            d = rng.randrange(1, min(n, len(out)) + 1)          # overlapping
+        else:
+            d = rng.randrange(n, min(len(out), 400) + 1) if len(out) >= n else len(out)
+        d = max(1, min(d, len(out)))
+        if r > 0.97:
+            s += bytes([((n - 1) << 2) | 3]) + d.to_bytes(4, "little")
+        elif d < 2048 and 4 <= n <= 11 and r < 0.7:
+            s += bytes([1 | ((n - 4) << 2) | ((d >> 8) << 5), d & 255])
+        else:
+            s += bytes([((n - 1) << 2) | 2, d & 255, d >> 8])
+        for k in range(n):
+            out.append(out[len(out) - d])
+    return _varint(len(out)) + bytes(s), bytes(out)
+
+
+@pytest.mark.parametrize("wide", ["trips", "walk"])
+def test_decode_wide_dependent_copies_and_c3(gpu, digests, force, wide):
+    # The wide class (outputs over 16 KiB) on C3 (its 64 KiB fillseq and
+    # random classes among the others) and on hand-made streams dense in
+    # copies that read this trip's own output, against the reference.
+    import random
+    import torch
+    from lcdb_amd import batch
+    force("wide", wide)
+    d = digests["C3_mixed"]
+    c = corpus.mixed()
+    raw = batch.upload(c)
+    comp = batch.encode_slots(raw)
+    batch.encode(raw, comp)
+    out = batch.decode_slots(c.len)
+    st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+    batch.decode(comp, out, st)
+    torch.cuda.synchronize()
+    assert bool((st == 1).all())
+    assert batch.digest(out) == (d["raw_sha256"], d["raw_bytes"])
+    rng = random.Random(2027)
+    ref = oracle.best()
+    streams, exps = [], []
+    for want in (17000, 40000, 65536, 66000, 120000):
+        for _ in range(3):
+            s, o = _trip_stress_stream(rng, want)
+            assert ref.decode(s) == o
+            streams += [s, s[:-1]]
+            exps += [o, ref.decode(s[:-1])]
+            k = rng.randrange(len(s) // 2, len(s))
+            bad = s[:k] + bytes([rng.randrange(256)]) + s[k + 1:]
+            streams.append(bad)
+            exps.append(ref.decode(bad))
+    res, st = gpu.decode_batch_host(streams, [1 << 18] * len(streams))
+    for k, (o, code, exp) in enumerate(zip(res, st, exps)):
+        if exp is None:
+            assert code == gpu.LGS_ST_CORRUPT, k
+        else:
+            assert code == gpu.LGS_ST_OK and o == exp, k

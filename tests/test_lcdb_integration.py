@@ -233,6 +233,7 @@ def test_c5_batched_table_write_and_read(gpu, c5_gpu_table, digests):
     f = out / "000001.ldb"
     assert f.stat().st_size == d["file_size"] and _sha256(f) == d["sha256"]
     _record(batched_process_seconds=round(wall, 1),
-            **{f"batched_{k}": fields[k] for k in ("blocks", "raw_bytes", "cut_s", "write_s",
-                                                   "finish_s", "io_s", "read_s")})
+            **{f"batched_{k}": fields[k] for k in ("blocks", "raw_bytes", "cut_s", "init_s",
+                                                   "write_s", "write_warm_s", "finish_s",
+                                                   "io_s", "read_s")})
     f.unlink()
