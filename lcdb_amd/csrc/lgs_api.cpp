@@ -1167,80 +1167,91 @@ int lgs_table_write_host(const uint8_t* raw, const uint64_t* raw_off, const uint
   }
   // Chunks of consecutive blocks are framed independently at file offset 0
   // (a block's framing does not depend on where it lands) and placed at
-  // their running offset when they come back.
+  // their running offset when they come back.  The staging is two slots,
+  // each sized for the largest chunk, used by alternate chunks: the pinned
+  // and device arenas stay bounded by the chunk size (LGS_HOST_CHUNK_MB),
+  // not by the call, so a multi-GiB table does not pin its whole image.
   const std::vector<uint32_t> first = chunk_bounds(n, in_total, raw_len);
   const uint32_t chunks = (uint32_t)first.size() - 1;
-  std::vector<size_t> fo(chunks + 1, 0);   // each chunk's file-region bound in the arena
   uint32_t max_n = 0;
+  size_t max_inb = 0, max_fo = 0;
   uint64_t max_raw = 0;
   for (uint32_t k = 0; k < chunks; ++k) {
     uint64_t r = 0;
-    for (uint32_t i = first[k]; i < first[k + 1]; ++i) r += raw_len[i];
-    fo[k + 1] = fo[k] + align_up((size_t)r + LGS_TRAILER_SIZE * (first[k + 1] - first[k]) + 16, 256);
-    if (first[k + 1] - first[k] > max_n) max_n = first[k + 1] - first[k];
+    size_t ib = 0;
+    for (uint32_t i = first[k]; i < first[k + 1]; ++i) {
+      r += raw_len[i];
+      ib += align_up(raw_len[i], 16);
+    }
+    const uint32_t m = first[k + 1] - first[k];
+    const size_t fo = align_up((size_t)r + LGS_TRAILER_SIZE * (size_t)m + 16, 256);
+    if (m > max_n) max_n = m;
     if (r > max_raw) max_raw = r;
+    if (ib > max_inb) max_inb = ib;
+    if (fo > max_fo) max_fo = fo;
   }
   const WriteScratch W(max_n, max_raw + 16 * (uint64_t)max_n);
-  Layout L;  // uploads | downloads | device-only
-  const size_t o_in = L.take(in_total + 16);
-  const size_t o_ioff = L.take(8 * (size_t)n);
-  const size_t o_ilen = L.take(4 * (size_t)n);
-  const size_t o_hoff = L.take(8 * (size_t)n);
-  const size_t o_hsize = L.take(8 * (size_t)n);
-  const size_t o_end = L.take(8 * (size_t)chunks);
-  const size_t o_file = L.take(fo[chunks]);
-  const size_t pin_end = L.at;
-  const size_t o_scr = L.take(2 * align_up(W.total, 256));
-  LGS_TRY(ctx_reserve(c, L.at, pin_end));
-  uint8_t* h = c.h_buf;
-  uint8_t* d = c.d_buf;
-  uint64_t* ioff = (uint64_t*)(h + o_ioff);
-  uint32_t* ilen = (uint32_t*)(h + o_ilen);
-  size_t ia = o_in;
-  for (uint32_t i = 0; i < n; ++i) {
-    ioff[i] = ia;
-    ilen[i] = raw_len[i];
-    ia += align_up(raw_len[i], 16);
-  }
+  Layout L;  // one slot: uploads | downloads | device-only
+  const size_t o_in = L.take(max_inb + 16);
+  const size_t o_ioff = L.take(8 * (size_t)max_n);
+  const size_t o_ilen = L.take(4 * (size_t)max_n);
+  const size_t o_hoff = L.take(8 * (size_t)max_n);
+  const size_t o_hsize = L.take(8 * (size_t)max_n);
+  const size_t o_end = L.take(8);
+  const size_t o_file = L.take(max_fo);
+  const size_t pin_slot = L.at;
+  const size_t o_scr = L.take(W.total);
+  const size_t dev_slot = L.at;
+  const uint32_t nslot = chunks > 1 ? 2 : 1;
+  LGS_TRY(ctx_reserve(c, nslot * dev_slot, nslot * pin_slot));
   uint64_t at = base;                      // file offset of the next chunk
   auto stage = [&](uint32_t k) {
-    par_for(first[k + 1] - first[k], ioff[first[k + 1] - 1] + 16 - ioff[first[k]],
-            [&](uint32_t j0, uint32_t j1) {
-              for (uint32_t i = first[k] + j0; i < first[k] + j1; ++i)
-                memcpy(h + ioff[i], raw + raw_off[i], raw_len[i]);
-            });
+    uint8_t* h = c.h_buf + (k & 1) * pin_slot;
+    uint64_t* ioff = (uint64_t*)(h + o_ioff);
+    uint32_t* ilen = (uint32_t*)(h + o_ilen);
+    size_t ia = o_in;
+    for (uint32_t i = first[k]; i < first[k + 1]; ++i) {
+      ioff[i - first[k]] = ia;
+      ilen[i - first[k]] = raw_len[i];
+      ia += align_up(raw_len[i], 16);
+    }
+    par_for(first[k + 1] - first[k], ia - o_in, [&](uint32_t j0, uint32_t j1) {
+      for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t i = first[k] + j;
+        memcpy(h + ioff[j], raw + raw_off[i], raw_len[i]);
+      }
+    });
   };
   auto launch = [&](uint32_t k, hipStream_t s) -> int {
-    const uint32_t i0 = first[k], m = first[k + 1] - i0;
-    const size_t a0 = ioff[i0], a1 = ioff[first[k + 1] - 1] + align_up(raw_len[first[k + 1] - 1], 16);
-    LGS_HIP(hipMemcpyAsync(d + a0, h + a0, a1 - a0, hipMemcpyHostToDevice, s));
-    LGS_HIP(hipMemcpyAsync(d + o_ioff + 8 * (size_t)i0, h + o_ioff + 8 * (size_t)i0, 8 * (size_t)m,
-                           hipMemcpyHostToDevice, s));
-    LGS_HIP(hipMemcpyAsync(d + o_ilen + 4 * (size_t)i0, h + o_ilen + 4 * (size_t)i0, 4 * (size_t)m,
-                           hipMemcpyHostToDevice, s));
-    uint8_t* scr = d + o_scr + (k & 1) * align_up(W.total, 256);
-    LGS_TRY(table_write(d, (const uint64_t*)(d + o_ioff) + i0, (const uint32_t*)(d + o_ilen) + i0,
-                        m, max_in, compression, 0, d + o_file + fo[k],
-                        (uint64_t*)(d + o_hoff) + i0, (uint64_t*)(d + o_hsize) + i0,
-                        (uint64_t*)(d + o_end) + k, scr, W, s));
-    LGS_HIP(hipMemcpyAsync(h + o_hoff + 8 * (size_t)i0, d + o_hoff + 8 * (size_t)i0,
-                           8 * (size_t)m, hipMemcpyDeviceToHost, s));
-    LGS_HIP(hipMemcpyAsync(h + o_hsize + 8 * (size_t)i0, d + o_hsize + 8 * (size_t)i0,
-                           8 * (size_t)m, hipMemcpyDeviceToHost, s));
-    LGS_HIP(hipMemcpyAsync(h + o_end + 8 * (size_t)k, d + o_end + 8 * (size_t)k, 8,
-                           hipMemcpyDeviceToHost, s));
+    uint8_t* h = c.h_buf + (k & 1) * pin_slot;
+    uint8_t* d = c.d_buf + (k & 1) * dev_slot;
+    const uint32_t m = first[k + 1] - first[k];
+    const uint64_t* ioff = (const uint64_t*)(h + o_ioff);
+    const size_t a1 = ioff[m - 1] + align_up(raw_len[first[k + 1] - 1], 16);
+    LGS_HIP(hipMemcpyAsync(d + o_in, h + o_in, a1 - o_in, hipMemcpyHostToDevice, s));
+    LGS_HIP(hipMemcpyAsync(d + o_ioff, h + o_ioff, 8 * (size_t)m, hipMemcpyHostToDevice, s));
+    LGS_HIP(hipMemcpyAsync(d + o_ilen, h + o_ilen, 4 * (size_t)m, hipMemcpyHostToDevice, s));
+    LGS_TRY(table_write(d, (const uint64_t*)(d + o_ioff), (const uint32_t*)(d + o_ilen), m, max_in,
+                        compression, 0, d + o_file, (uint64_t*)(d + o_hoff),
+                        (uint64_t*)(d + o_hsize), (uint64_t*)(d + o_end), d + o_scr, W, s));
+    LGS_HIP(hipMemcpyAsync(h + o_hoff, d + o_hoff, 8 * (size_t)m, hipMemcpyDeviceToHost, s));
+    LGS_HIP(hipMemcpyAsync(h + o_hsize, d + o_hsize, 8 * (size_t)m, hipMemcpyDeviceToHost, s));
+    LGS_HIP(hipMemcpyAsync(h + o_end, d + o_end, 8, hipMemcpyDeviceToHost, s));
     // The region's size is known only on the device: its bound comes back.
-    LGS_HIP(hipMemcpyAsync(h + o_file + fo[k], d + o_file + fo[k], fo[k + 1] - fo[k],
-                           hipMemcpyDeviceToHost, s));
+    uint64_t r = 0;
+    for (uint32_t i = first[k]; i < first[k + 1]; ++i) r += raw_len[i];
+    const size_t fo = align_up((size_t)r + LGS_TRAILER_SIZE * (size_t)m + 16, 256);
+    LGS_HIP(hipMemcpyAsync(h + o_file, d + o_file, fo, hipMemcpyDeviceToHost, s));
     return LGS_OK;
   };
   auto finish = [&](uint32_t k) -> int {
+    const uint8_t* h = c.h_buf + (k & 1) * pin_slot;
     const uint32_t i0 = first[k], m = first[k + 1] - i0;
-    const uint64_t bytes = ((const uint64_t*)(h + o_end))[k];
+    const uint64_t bytes = *(const uint64_t*)(h + o_end);
     if (at - base + bytes > file_cap)
       return fail(LGS_EINVAL, "file buffer of %zu bytes, %zu needed", file_cap,
                   (size_t)(at - base + bytes));
-    const uint8_t* src = h + o_file + fo[k];
+    const uint8_t* src = h + o_file;
     uint8_t* dst = file + (at - base);
     const uint32_t parts = 64;
     const size_t per = ((size_t)bytes + parts - 1) / parts;
@@ -1248,8 +1259,8 @@ int lgs_table_write_host(const uint8_t* raw, const uint64_t* raw_off, const uint
       const size_t x0 = (size_t)q0 * per, x1 = (size_t)q1 * per < bytes ? (size_t)q1 * per : bytes;
       if (x0 < x1) memcpy(dst + x0, src + x0, x1 - x0);
     });
-    const uint64_t* ho = (const uint64_t*)(h + o_hoff) + i0;
-    const uint64_t* hs = (const uint64_t*)(h + o_hsize) + i0;
+    const uint64_t* ho = (const uint64_t*)(h + o_hoff);
+    const uint64_t* hs = (const uint64_t*)(h + o_hsize);
     for (uint32_t j = 0; j < m; ++j) {
       handle_off[i0 + j] = ho[j] + at;
       handle_size[i0 + j] = hs[j];
@@ -1272,101 +1283,110 @@ int lgs_table_read_host(const uint8_t* file, uint64_t file_len, const uint64_t* 
   Lease lease(batch_pool());
   LGS_TRY(lease.acquire());
   Ctx& c = lease.ctx();
-  // Only each block's byte range (+ trailer) travels, packed 16-aligned;
-  // a range outside the file keeps an out-of-range offset so the device
-  // reports the truncated read itself (format.c:195-198).
-  size_t blk_total = 0, out_total = 0;
+  // Only each block's byte range (+ trailer) travels, packed 16-aligned into
+  // its chunk's image; a range outside the file keeps an offset past that
+  // image, so the device reports the truncated read itself (format.c:195-198).
+  auto in_file = [&](uint32_t i) {
+    const uint64_t o = handle_off[i], sz = handle_size[i];
+    return sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE;
+  };
+  size_t out_total = 0;
   uint32_t max_cap = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t o = handle_off[i], sz = handle_size[i];
-    if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE)
-      blk_total += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
     out_total += align_up(out_cap[i], 16);
     if (out_cap[i] > max_cap) max_cap = out_cap[i];
   }
-  // Chunks of consecutive handles go through the two-stream pipeline (see
-  // pipeline()); each chunk's packed ranges are contiguous in the image.
+  // Chunks of consecutive handles through the two-stream pipeline (see
+  // pipeline()), staged in two slots sized for the largest chunk (bounded
+  // by LGS_HOST_CHUNK_MB, not by the call; see lgs_table_write_host).
   const std::vector<uint32_t> first = chunk_bounds(n, out_total, out_cap);
   const uint32_t chunks = (uint32_t)first.size() - 1;
   uint32_t max_n = 0;
-  for (uint32_t k = 0; k < chunks; ++k)
-    if (first[k + 1] - first[k] > max_n) max_n = first[k + 1] - first[k];
-  const ReadScratch R(max_n);
-  Layout L;
-  const size_t o_blk = L.take(blk_total + 16);
-  const size_t o_hoff = L.take(8 * (size_t)n);
-  const size_t o_hsize = L.take(8 * (size_t)n);
-  const size_t o_ooff = L.take(8 * (size_t)n);
-  const size_t o_ocap = L.take(4 * (size_t)n);
-  const size_t o_st = L.take((size_t)n);
-  const size_t o_olen = L.take(4 * (size_t)n);
-  const size_t o_out = L.take(out_total + 16);
-  const size_t pin_end = L.at;
-  const size_t o_scr = L.take(2 * align_up(R.total, 256));
-  LGS_TRY(ctx_reserve(c, L.at, pin_end));
-  uint8_t* h = c.h_buf;
-  uint8_t* d = c.d_buf;
-  uint64_t* hoff = (uint64_t*)(h + o_hoff);
-  uint64_t* hsize = (uint64_t*)(h + o_hsize);
-  uint64_t* ooff = (uint64_t*)(h + o_ooff);
-  uint32_t* ocap = (uint32_t*)(h + o_ocap);
-  std::vector<size_t> pa(chunks + 1, 0);     // each chunk's packed range in the image
-  size_t ba = 0, oa = o_out;
-  const uint64_t img_len = blk_total + 16;   // device file image: the packed ranges
+  size_t max_blk = 0, max_out = 0;
   for (uint32_t k = 0; k < chunks; ++k) {
-    pa[k] = ba;
+    size_t bb = 0, ob = 0;
     for (uint32_t i = first[k]; i < first[k + 1]; ++i) {
-      const uint64_t o = handle_off[i], sz = handle_size[i];
-      hsize[i] = sz;
-      if (sz <= ~0ull - LGS_TRAILER_SIZE && o <= file_len && file_len - o >= sz + LGS_TRAILER_SIZE) {
-        hoff[i] = ba;
-        ba += align_up((size_t)sz + LGS_TRAILER_SIZE, 16);
-      } else {
-        hoff[i] = img_len + 1;
-      }
-      ooff[i] = oa;
-      ocap[i] = out_cap[i];
+      if (in_file(i)) bb += align_up((size_t)handle_size[i] + LGS_TRAILER_SIZE, 16);
+      ob += align_up(out_cap[i], 16);
+    }
+    if (first[k + 1] - first[k] > max_n) max_n = first[k + 1] - first[k];
+    if (bb > max_blk) max_blk = bb;
+    if (ob > max_out) max_out = ob;
+  }
+  const ReadScratch R(max_n);
+  Layout L;  // one slot
+  const size_t o_blk = L.take(max_blk + 16);
+  const size_t o_hoff = L.take(8 * (size_t)max_n);
+  const size_t o_hsize = L.take(8 * (size_t)max_n);
+  const size_t o_ooff = L.take(8 * (size_t)max_n);
+  const size_t o_ocap = L.take(4 * (size_t)max_n);
+  const size_t o_st = L.take((size_t)max_n);
+  const size_t o_olen = L.take(4 * (size_t)max_n);
+  const size_t o_out = L.take(max_out + 16);
+  const size_t pin_slot = L.at;
+  const size_t o_scr = L.take(R.total);
+  const size_t dev_slot = L.at;
+  const uint32_t nslot = chunks > 1 ? 2 : 1;
+  LGS_TRY(ctx_reserve(c, nslot * dev_slot, nslot * pin_slot));
+  std::vector<size_t> blk_len(chunks, 0);   // each chunk's packed image length
+  auto stage = [&](uint32_t k) {
+    uint8_t* h = c.h_buf + (k & 1) * pin_slot;
+    uint64_t* hoff = (uint64_t*)(h + o_hoff);
+    uint64_t* hsize = (uint64_t*)(h + o_hsize);
+    uint64_t* ooff = (uint64_t*)(h + o_ooff);
+    uint32_t* ocap = (uint32_t*)(h + o_ocap);
+    size_t ba = 0, oa = o_out;
+    const uint32_t i0 = first[k], m = first[k + 1] - i0;
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint32_t i = i0 + j;
+      hsize[j] = handle_size[i];
+      hoff[j] = in_file(i) ? ba : ~0ull;
+      if (in_file(i)) ba += align_up((size_t)handle_size[i] + LGS_TRAILER_SIZE, 16);
+      ooff[j] = oa;
+      ocap[j] = out_cap[i];
       oa += align_up(out_cap[i], 16);
     }
-  }
-  pa[chunks] = ba;
-  auto stage = [&](uint32_t k) {
-    par_for(first[k + 1] - first[k], pa[k + 1] - pa[k], [&](uint32_t j0, uint32_t j1) {
-      for (uint32_t i = first[k] + j0; i < first[k] + j1; ++i)
-        if (hoff[i] <= img_len)
-          memcpy(h + o_blk + hoff[i], file + handle_off[i], (size_t)hsize[i] + LGS_TRAILER_SIZE);
+    blk_len[k] = ba;
+    for (uint32_t j = 0; j < m; ++j)
+      if (hoff[j] == ~0ull) hoff[j] = ba + 16 + 1;   // past the image: a truncated read
+    par_for(m, ba, [&](uint32_t j0, uint32_t j1) {
+      for (uint32_t j = j0; j < j1; ++j)
+        if (hoff[j] <= ba)
+          memcpy(h + o_blk + hoff[j], file + handle_off[i0 + j], (size_t)hsize[j] + LGS_TRAILER_SIZE);
     });
   };
   auto launch = [&](uint32_t k, hipStream_t s) -> int {
-    const uint32_t i0 = first[k], m = first[k + 1] - i0, il = first[k + 1] - 1;
-    if (pa[k + 1] > pa[k])
-      LGS_HIP(hipMemcpyAsync(d + o_blk + pa[k], h + o_blk + pa[k], pa[k + 1] - pa[k],
-                             hipMemcpyHostToDevice, s));
+    uint8_t* h = c.h_buf + (k & 1) * pin_slot;
+    uint8_t* d = c.d_buf + (k & 1) * dev_slot;
+    const uint32_t m = first[k + 1] - first[k];
+    const uint64_t* ooff = (const uint64_t*)(h + o_ooff);
+    if (blk_len[k] > 0)
+      LGS_HIP(hipMemcpyAsync(d + o_blk, h + o_blk, blk_len[k], hipMemcpyHostToDevice, s));
     for (const size_t o : {o_hoff, o_hsize, o_ooff})
-      LGS_HIP(hipMemcpyAsync(d + o + 8 * (size_t)i0, h + o + 8 * (size_t)i0, 8 * (size_t)m,
-                             hipMemcpyHostToDevice, s));
-    LGS_HIP(hipMemcpyAsync(d + o_ocap + 4 * (size_t)i0, h + o_ocap + 4 * (size_t)i0,
-                           4 * (size_t)m, hipMemcpyHostToDevice, s));
-    uint8_t* scr = d + o_scr + (k & 1) * align_up(R.total, 256);
-    LGS_TRY(table_read(d + o_blk, img_len, (const uint64_t*)(d + o_hoff) + i0,
-                       (const uint64_t*)(d + o_hsize) + i0, m, verify_checksums, d,
-                       (const uint64_t*)(d + o_ooff) + i0, (const uint32_t*)(d + o_ocap) + i0,
-                       max_cap, (uint32_t*)(d + o_olen) + i0, d + o_st + i0, scr, R, s));
-    LGS_HIP(hipMemcpyAsync(h + o_st + i0, d + o_st + i0, m, hipMemcpyDeviceToHost, s));
-    LGS_HIP(hipMemcpyAsync(h + o_olen + 4 * (size_t)i0, d + o_olen + 4 * (size_t)i0,
-                           4 * (size_t)m, hipMemcpyDeviceToHost, s));
-    const size_t oe = ooff[il] + align_up(out_cap[il], 16);
-    LGS_HIP(hipMemcpyAsync(h + ooff[i0], d + ooff[i0], oe - ooff[i0], hipMemcpyDeviceToHost, s));
+      LGS_HIP(hipMemcpyAsync(d + o, h + o, 8 * (size_t)m, hipMemcpyHostToDevice, s));
+    LGS_HIP(hipMemcpyAsync(d + o_ocap, h + o_ocap, 4 * (size_t)m, hipMemcpyHostToDevice, s));
+    LGS_TRY(table_read(d + o_blk, blk_len[k] + 16, (const uint64_t*)(d + o_hoff),
+                       (const uint64_t*)(d + o_hsize), m, verify_checksums, d,
+                       (const uint64_t*)(d + o_ooff), (const uint32_t*)(d + o_ocap), max_cap,
+                       (uint32_t*)(d + o_olen), d + o_st, d + o_scr, R, s));
+    LGS_HIP(hipMemcpyAsync(h + o_st, d + o_st, m, hipMemcpyDeviceToHost, s));
+    LGS_HIP(hipMemcpyAsync(h + o_olen, d + o_olen, 4 * (size_t)m, hipMemcpyDeviceToHost, s));
+    const size_t oe = ooff[m - 1] + align_up(out_cap[first[k + 1] - 1], 16);
+    LGS_HIP(hipMemcpyAsync(h + o_out, d + o_out, oe - o_out, hipMemcpyDeviceToHost, s));
     return LGS_OK;
   };
   auto finish = [&](uint32_t k) -> int {
+    const uint8_t* h = c.h_buf + (k & 1) * pin_slot;
+    const uint32_t i0 = first[k], m = first[k + 1] - i0;
     const uint32_t* olen = (const uint32_t*)(h + o_olen);
-    const size_t bytes = ooff[first[k + 1] - 1] + out_cap[first[k + 1] - 1] - ooff[first[k]];
-    par_for(first[k + 1] - first[k], bytes, [&](uint32_t j0, uint32_t j1) {
-      for (uint32_t i = first[k] + j0; i < first[k] + j1; ++i) {
-        status[i] = h[o_st + i];
-        out_len[i] = olen[i];
-        if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[i], olen[i]);
+    const uint64_t* ooff = (const uint64_t*)(h + o_ooff);
+    const size_t bytes = ooff[m - 1] + out_cap[first[k + 1] - 1] - ooff[0];
+    par_for(m, bytes, [&](uint32_t j0, uint32_t j1) {
+      for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t i = i0 + j;
+        status[i] = h[o_st + j];
+        out_len[i] = olen[j];
+        if (status[i] == LGS_ST_OK) memcpy(out + out_off[i], h + ooff[j], olen[j]);
       }
     });
     return LGS_OK;

@@ -330,6 +330,24 @@ def test_host_paths_chunked_c2_scale(tab):
     res, st = tab.read_blocks_host(image, hoff, hsize, [int(x) for x in c.len])
     assert all(int(x) == tab.LGS_ST_OK for x in st)
     assert res == blocks
+    # Bad handles and a damaged block in different chunks of the pipeline
+    # (each chunk stages its own image): the reference's outcome for each.
+    hoff2, hsize2 = hoff.copy(), hsize.copy()
+    hoff2[5] = len(image) + 100                        # past the end
+    hsize2[20000] = len(image)                         # runs past the end
+    hoff2[40000] = len(image) - 3                      # trailer cut off
+    img2 = bytearray(image)
+    img2[int(hoff[65535]) + 2] ^= 0x10                 # checksum mismatch
+    img2 = bytes(img2)
+    res, st = tab.read_blocks_host(img2, hoff2, hsize2, [int(x) for x in c.len], True)
+    for i in range(c.n):
+        if i in (5, 20000, 40000, 65535):
+            ost, ores = oracle.table_read_block(img2, int(hoff2[i]), int(hsize2[i]), True,
+                                                int(c.len[i]))
+            assert int(st[i]) == ost and res[i] == ores, i
+            assert ost != tab.LGS_ST_OK, i
+        else:
+            assert int(st[i]) == tab.LGS_ST_OK and res[i] == blocks[i], i
 
 
 def test_write_then_read_device_c2_scale(tab):
