@@ -531,6 +531,9 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     const uint32_t hh = valid ? hash32(xv, shift) : kSink;
     // snappy.c:146-148 (and :175, :179 for A and B) for all 64 probes at once.
     uint32_t prev = tab_swap(tab, hh, p);
+    // The candidate's bytes are read before the order check, so the check
+    // runs under the read's latency (the rare path reads them again).
+    uint32_t yv = x.rd32(valid ? prev : 0);
     if (ballot(valid & (prev > p))) {
       // Not in lane order (never seen on gfx950): put back each touched
       // slot's entry as the batch found it (the one lane per slot that
@@ -543,8 +546,8 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
         const uint32_t got = tab_swap(tab, lane == l ? hh : kSink, p);
         prev = lane == l ? got : prev;
       }
+      yv = x.rd32(valid ? prev : 0);
     }
-    uint32_t yv = x.rd32(valid ? prev : 0);
     if constexpr (IN::kWin) {
       const bool oc = valid & x.oow(prev, 4);
       if (ballot(oc)) yv = oc ? x.g32(prev) : yv;
