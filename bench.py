@@ -577,7 +577,8 @@ def cpu_baseline(c, a, gpu_comp, world: int) -> dict:
 
     pts = {t: point(t) for t in counts}
     # the headline: the fastest point (the whole node's CPUs, nproc, unless
-    # fewer threads do better on this sample)
+    # fewer threads do better on this sample -- as on a shared GPU box whose
+    # container is held to a CPU quota, reported as cgroup_cpu_quota)
     top = max(pts.values(), key=lambda x: x["roundtrip_GiBps"])
     host = oracle.cpu_model()
     return {"value": top["roundtrip_GiBps"], "unit": "GiB/s", "cores": top["cores"],
@@ -587,8 +588,8 @@ def cpu_baseline(c, a, gpu_comp, world: int) -> dict:
             "cpu_model": host["model"], "physical_cores": host["physical_cores"],
             "logical_cpus": host["logical_cpus"], "affinity_cpus": host["affinity_cpus"],
             "affinity_physical_cores": host["affinity_physical_cores"],
-            "numa_nodes": host["numa_nodes"], "gpus_in_this_run": world,
-            "same_bytes_as_gpu": same,
+            "numa_nodes": host["numa_nodes"], "cgroup_cpu_quota": host["cgroup_cpu_quota"],
+            "gpus_in_this_run": world, "same_bytes_as_gpu": same,
             "sample": f"first {m} of rank 0's blocks ({plan['raw_bytes']} B raw), encode then "
                       f"decode, warm-up + median of {a.cpu_reps} runs, at {counts} threads "
                       f"(round-robin and contiguous partitions, NUMA-local outputs)"}

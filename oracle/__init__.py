@@ -424,7 +424,29 @@ def cpu_model() -> dict:
         numa = None
     return {"model": model, "physical_cores": len(phys) or None,
             "logical_cpus": os.cpu_count(), "affinity_cpus": len(aff),
-            "affinity_physical_cores": _affinity_cores(aff), "numa_nodes": numa}
+            "affinity_physical_cores": _affinity_cores(aff), "numa_nodes": numa,
+            "cgroup_cpu_quota": cgroup_cpu_quota()}
+
+
+def cgroup_cpu_quota() -> float | None:
+    """CPUs' worth of time this process's cgroup may use (cgroup v2 cpu.max,
+    or v1 cfs_quota/cfs_period), None when unlimited or unknown.  A shared GPU
+    box can show every CPU in the affinity mask while capping the container
+    at its share: threads beyond the quota only time-slice."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
 
 
 def baseline_plan(codec: Codec, buf, off, ln, thread_counts, reps: int = 5,
