@@ -380,3 +380,42 @@ def test_write_then_read_device_c2_scale(tab):
     k = 512
     want = oracle.table_write_blocks([c.block(i) for i in range(k)], 1, 0)
     assert d_file[:want[3]].cpu().numpy().tobytes() == want[0]
+
+
+_SMALL_CHUNKS = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import oracle
+from lcdb_amd import corpus, table
+c = corpus.concat(corpus.fillseq(1500), corpus.random_blocks(301, 4096),
+                  corpus.fillseq(7, block_size=65536))
+blocks = c.blocks()
+region, hoff, hsize, end = table.write_blocks_host(blocks, table.LGS_SNAPPY_COMPRESSION, 5)
+assert end == 5 + len(region)
+ref = oracle.table_write_blocks(blocks, 1, 5)
+assert bytes(region) == ref[0], "region differs from the oracle"
+assert np.array_equal(np.asarray(hoff, dtype=np.uint64), ref[1])
+image = b"\0" * 5 + bytes(region)
+res, st = table.read_blocks_host(image, hoff, hsize, [int(x) for x in c.len])
+assert all(int(x) == table.LGS_ST_OK for x in st) and res == blocks
+print("chunks ok", len(blocks))
+"""
+
+
+def test_host_paths_many_small_chunks(gpu, tmp_path):
+    """LGS_HOST_CHUNK_MB=1 (read once at load, so in a child process): the
+    table host paths run ~10 chunks through their two staging slots, an odd
+    number, with 4 KiB and 64 KiB blocks; the region equals the oracle's
+    framing byte for byte and every block reads back."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "small_chunks.py"
+    script.write_text(_SMALL_CHUNKS)
+    env = dict(os.environ, LGS_HOST_CHUNK_MB="1", PYTHONPATH=os.path.join(root, "tests"))
+    r = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "chunks ok 1808" in r.stdout
