@@ -306,7 +306,10 @@ int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
                          size_t *slot_bytes);
 
 /* Process-wide kernel choices (A/B and tests; the defaults pick by batch):
-     "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
+     "decoder": "auto" | "ops" (two passes: a lane per block walks the tags
+                into op lists, a wave per block executes them; outputs of
+                the 4 608-byte class, larger ones go to the defaults)
+                | "ring" (lane-per-block) | "wave" (wave-per-block)
                 | "quad" (four lanes per block; A/B only)
      "wide":    "walk" (default) | "trips"  (decoder of outputs over 16 KiB:
                 the one-tag walk, or up to 8 tags per step; A/B only)

@@ -728,6 +728,7 @@ Options& options_init() {
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
     if (dk && !strcmp(dk, "quad")) v->decoder = kDecQuad;
+    if (dk && !strcmp(dk, "ops")) v->decoder = kDecOps;
     const char* ns = getenv("LGS_NO_SPLIT");
     if (ns && *ns && strcmp(ns, "0")) v->split = 0;
     const char* wd = getenv("LGS_WIDE_DECODER");
@@ -804,7 +805,8 @@ int lgs_set_option(const char* name, const char* value) {
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
     else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring, quad or wave)", value);
+    else if (!strcmp(value, "ops")) o.decoder = kDecOps;
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ops, ring, quad or wave)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)

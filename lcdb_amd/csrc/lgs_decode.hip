@@ -2002,7 +2002,427 @@ hipError_t launch_decode_quad(const DecodeArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Two-pass decoder (round 3): large batches of small blocks (outputs of the
+// 4 608-byte class; C2, C4).
+//
+// The ring decoder's time is one wave's serial stream of walk *and* byte
+// moves (~340 instructions per tag step at ~10 cycles each).
+// Here the two are split over two kernels with the op list in HBM between:
+//
+//   pass 1, tag_scan_kernel: one lane per block walks the block's tags
+//     (snappy.c:208-324, every reject in the reference's order) and writes
+//     one 4-byte record per op.  The walk reads its stream from a 512-byte
+//     LDS ring per lane that LDS-DMA loads (global_load_lds) fill one
+//     256-byte segment ahead, so a step waits on LDS, never on HBM; the
+//     walk moves no output byte, so a step is ~50 instructions.
+//   pass 2, op_exec_kernel: one wave per block executes the block's records
+//     64 at a time in an LDS image of the output: every literal at once
+//     (16 bytes a lane, read from the stream in HBM), then every copy whose
+//     source holds no byte of an earlier copy of the batch at once, then the
+//     remaining copies in order; the image is written out whole.
+//
+// Record (bit 31 = copy): a literal is (len - 1) << 17 | its first byte's
+// stream offset; a copy 1 << 31 | (len - 1) << 17 | distance.  Output
+// offsets are the running sum of the lengths (pass 2 scans them).  A block
+// with more than kK ops (average op under 4.5 bytes: only synthetic
+// streams) is decoded by pass 2 from its stream alone (decode_stream), as is
+// one whose stream is too long for the 17-bit offsets.
+// ---------------------------------------------------------------------------
+namespace ops {
+constexpr uint32_t kSeg = 256;        // stream bytes per ring segment; two per lane
+constexpr uint32_t kK = 1024;         // records per block
+constexpr uint32_t kOut = 4608;       // output class
+constexpr uint32_t kMaxStream = 131072 - 64;   // literal offsets fit 17 bits
+constexpr uint32_t kExec = 1u << 30, kSelf = 2u << 30;   // pass-2 states (meta.x top bits)
+#ifndef LGS_OPS_BL
+#define LGS_OPS_BL 64
+#endif
+constexpr uint32_t kBL = LGS_OPS_BL;  // blocks (lanes) per pass-1 wave
+}  // namespace ops
+
+// LDS-DMA: 16 bytes per active lane from gaddr to LDS byte address
+// lds_base + 16 * lane (global_load_lds_dwordx4).  Inline asm, so hipcc
+// neither counts it nor waits for it: the pass-1 walk tracks it itself.
+__device__ __forceinline__ void glds16(uint64_t gaddr, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep) : "v"(gaddr), "s"(lds_base) : "memory");
+}
+
+// s_waitcnt immediate for vmcnt(n) (gfx9: bits 3:0 and 15:14; lgkmcnt and
+// expcnt left at their maximum, i.e. not waited for).
+constexpr int vmcnt_imm(int n) { return 0x0f70 | (n & 15) | ((n >> 4) << 14); }
+
+// Wave-wide inclusive prefix sum / max (DPP: rows of 16, then the row
+// broadcasts of gfx9).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+  x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+// Value of x in the lane below (0 in lane 0): DPP wave_shr:1.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+}
+
+template <uint32_t BL>
+__global__ __launch_bounds__(64) void tag_scan_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n, const uint32_t* __restrict__ count,
+    uint32_t* __restrict__ rec, uint2* __restrict__ meta) {
+  using namespace ops;
+  // Half h of lane j's ring: s_ring[(h * BL + j) * kSeg ..].  Segment s (of
+  // the stream's 16-byte-aligned view) lives in half s & 1.
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[2 * BL * kSeg];
+  const uint32_t lane = threadIdx.x;
+  if (count) n = uni(*count);
+  if (blockIdx.x * BL >= n) return;
+  const uint32_t slot = blockIdx.x * BL + lane;
+  const bool exists = (lane < BL) & (slot < n);
+  const uint32_t i = exists ? (index ? index[slot] : slot) : 0;
+  const uint64_t sp = reinterpret_cast<uint64_t>(in) + (exists ? in_off[i] : 0);
+  const uint32_t slen = exists ? in_len[i] : 0;
+  const uint32_t cap = exists ? out_cap[i] : 0;
+  // Stream byte p is byte u = p + sh of the aligned view starting at gb.
+  const uint32_t sh = (uint32_t)sp & 15u;
+  const uint64_t gb = sp - sh;
+  const uint32_t lastg = slen ? (sh + slen - 1) >> 4 : 0;   // last granule holding a byte
+  const uint32_t ring0 = lds_addr(s_ring);
+  const uint8_t* const mine = s_ring + (lane < BL ? lane : 0) * kSeg;
+
+  // Vector-memory instructions issued (LDS-DMA and record stores: vmcnt
+  // counts both); every one below jret has completed.  jh0 / jh1: index of
+  // the last DMA into this lane's half 0 / 1.
+  uint32_t J = 0, jret = 0;
+  int32_t jh0 = -1, jh1 = -1;
+  // DMA of segment seg (per lane) for the lanes in m: one instruction per
+  // lane, 16 lanes x 16 bytes, granules clamped to the stream's last.
+  auto issue = [&](uint64_t m, uint32_t seg) {
+    for (; m; m &= m - 1) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      const uint32_t sj = lane_val(seg, j), lj = lane_val(lastg, j);
+      const uint64_t gj = ((uint64_t)lane_val((uint32_t)(gb >> 32), j) << 32) |
+                          lane_val((uint32_t)gb, j);
+      if (lane < 16) {
+        const uint32_t g = 16 * sj + lane;
+        glds16(gj + 16ull * (g < lj ? g : lj), ring0 + ((sj & 1) * BL + j) * kSeg);
+      }
+      const bool me = lane == j;
+      jh0 = (me & !(sj & 1)) ? (int32_t)J : jh0;
+      jh1 = (me & (sj & 1)) ? (int32_t)J : jh1;
+      ++J;
+    }
+  };
+  // Bytes u .. u+4 of the lane's view from its ring (two aligned dwords):
+  // x = bytes u..u+3, y's low byte = byte u+4.
+  auto rd = [&](uint32_t u, uint32_t* x, uint32_t* y) {
+    const uint32_t d0 = u & ~3u, d1 = d0 + 4;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(mine + ((d0 >> 8) & 1) * BL * kSeg + (d0 & 255));
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(mine + ((d1 >> 8) & 1) * BL * kSeg + (d1 & 255));
+    *x = __builtin_amdgcn_alignbyte(w1, w0, u & 3u);
+    *y = w1 >> (8 * (u & 3u));
+  };
+
+  issue(ballot(exists), 0u);
+  issue(ballot(exists & (lastg >= 16)), 1u);
+  __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
+  jret = J;
+
+  // varint32 header, coding.h:169-204.  st: 1 walking/ok, 0 corrupt,
+  // 2 no space, 3 no block, 4 decoded by pass 2 from the stream.
+  uint32_t st = exists ? 1u : 3u, want = 0, hlen = 0;
+  {
+    uint32_t x, y;
+    rd(sh, &x, &y);
+    for (uint32_t k = 0; k < 5; ++k) {
+      const uint32_t b = ((k < 4 ? x >> (8 * k) : y)) & 0xffu;
+      if (k < slen && hlen == 0) {
+        want |= (b & 0x7fu) << (7 * k);
+        if ((b & 0x80u) == 0) hlen = k + 1;
+      }
+    }
+    if (exists) {
+      if (hlen == 0 || want > 0x7fffffffu) st = 0;              // snappy.c:405-409
+      else if (want > cap) st = 2;
+      else if (slen > kMaxStream) st = 4;
+    }
+  }
+
+  uint32_t pos = hlen, made = 0, k = 0, segl = 0;
+  u32x4 rb = {0, 0, 0, 0};                                    // four records, then one store
+  gptr<u32x4> const rq = (gptr<u32x4>)(to_global(rec) + (size_t)slot * kK);
+  for (;;) {
+    const bool act = (st == 1) & (pos < slen);                // snappy.c:208
+    if (!ballot(act)) break;
+    const uint32_t u = pos + sh, s = u >> 8;
+    // Leaving segment segl: load segment s + 1 into the half just left
+    // (after a long literal: segments s and s + 1).
+    const bool adv = act & (s != segl);
+    if (ballot(adv)) {
+      const bool jump = s > segl + 1;
+      const uint32_t sa = jump ? s : s + 1;
+      issue(ballot(adv & (16 * sa <= lastg)), sa);
+      issue(ballot(adv & jump & (16 * (s + 1) <= lastg)), s + 1);
+      segl = adv ? s : segl;
+    }
+    // Keep at most 40 in flight, so everything issued before J - 40 has
+    // landed; wait further only for a half whose DMA may still be in flight.
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(40));
+    jret = J > 40 ? (J - 40 > jret ? J - 40 : jret) : jret;
+    const uint32_t e = ((u & ~3u) + 7) >> 8;
+    const int32_t ja = (s & 1) ? jh1 : jh0, jb = (e & 1) ? jh1 : jh0;
+    const int32_t jn = ja > jb ? ja : jb;
+    const bool pend = act & (jn >= (int32_t)jret);
+    if (ballot(pend)) {
+      int32_t top = -1;
+      for (uint64_t m = ballot(pend); m; m &= m - 1) {
+        const int32_t v = (int32_t)lane_val((uint32_t)jn, (uint32_t)__builtin_ctzll(m));
+        top = v > top ? v : top;
+      }
+      const uint32_t allow = J - 1 - (uint32_t)top;           // newer instructions that may stay
+      if (allow >= 16) {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(16));
+        jret = J - 16;
+      } else if (allow >= 4) {
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(4));
+        jret = J - 4;
+      } else {
+        __builtin_amdgcn_s_waitcnt(0x0f70);                   // vmcnt(0)
+        jret = J;
+      }
+    }
+    // The tag (snappy.c:210-324; parse_tag's folded rejects).
+    uint32_t x, y;
+    rd(u, &x, &y);
+    const uint32_t tag = x & 0xffu, kind = tag & 3u, m0 = tag >> 2;
+    const uint32_t left = slen - pos;
+    const uint32_t b1 = (x >> 8) | (y << 24);                   // bytes 1..4
+    const bool lit = kind == 0;
+    const uint32_t extra = m0 >= 60 ? m0 - 59 : 0u;
+    const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
+    const uint32_t m = extra ? (b1 & emask) : m0;
+    const uint32_t clen = kind == 1 ? 4 + (m0 & 7u) : m0 + 1;
+    const uint32_t cdist = kind == 1 ? ((tag & 0xe0u) << 3) | (b1 & 0xffu)
+                                     : (kind == 2 ? b1 & 0xffffu : b1);
+    const uint32_t len = lit ? m + 1 : clen;
+    const uint32_t hl = lit ? 1 + extra : (kind == 3 ? 5u : kind + 1);
+    const bool bad = (hl > left) | (len > want - made) |
+                     (lit ? (m >= 0x7fffffffu) | (hl + len > left) : (cdist - 1 >= made));
+    const bool take = act & !bad & (k < kK);
+    st = (act & bad) ? 0u : st;
+    st = (act & !bad & (k >= kK)) ? 4u : st;
+    const uint32_t r = lit ? ((len - 1) << 17) | (pos + hl)
+                           : 0x80000000u | ((len - 1) << 17) | cdist;
+    const uint32_t q = k & 3u;
+    rb.x = (take & (q == 0)) ? r : rb.x;
+    rb.y = (take & (q == 1)) ? r : rb.y;
+    rb.z = (take & (q == 2)) ? r : rb.z;
+    rb.w = (take & (q == 3)) ? r : rb.w;
+    const bool full = take & (q == 3);
+    if (ballot(full)) {
+      if (full) rq[k >> 2] = rb;
+      ++J;
+    }
+    k += take ? 1u : 0u;
+    made += take ? len : 0u;
+    pos += take ? hl + (lit ? len : 0u) : 0u;
+  }
+  if ((st == 1) & (made != want)) st = 0;                        // snappy.c:337
+  const bool part = (st == 1) & ((k & 3u) != 0);
+  if (part) rq[k >> 2] = rb;
+  if (exists) {
+    if (st == 1) {
+      meta[slot] = uint2{kExec | k, want};
+    } else if (st == 4) {
+      meta[slot] = uint2{kSelf, 0};
+    } else {
+      meta[slot] = uint2{0, 0};
+      status[i] = (uint8_t)st;
+      out_len[i] = 0;
+    }
+  }
+}
+
+// Exact-size LDS writes of the first t < 16 bytes of v at p (exec-masked).
+__device__ __forceinline__ void lds_exact(uint8_t* p, u32x4 v, uint32_t t) {
+  typedef uint64_t u64_a1 __attribute__((aligned(1)));
+  typedef uint32_t u32_a1 __attribute__((aligned(1)));
+  typedef uint16_t u16_a1 __attribute__((aligned(1)));
+  if (t & 8) {
+    *(u64_a1*)p = ((uint64_t)v.y << 32) | v.x;
+    v = u32x4{v.z, v.w, 0, 0};
+    p += 8;
+  }
+  if (t & 4) {
+    *(u32_a1*)p = v.x;
+    v.x = v.y;
+    p += 4;
+  }
+  if (t & 2) {
+    *(u16_a1*)p = (uint16_t)v.x;
+    v.x >>= 16;
+    p += 2;
+  }
+  if (t & 1) *p = (uint8_t)v.x;
+}
+
+// Up to 64 bytes (c0..c3) at p: whole 16-byte pieces, then the exact tail.
+__device__ __forceinline__ void lds_put64(uint8_t* p, uint32_t n, bool on, u32x4 c0, u32x4 c1,
+                                          u32x4 c2, u32x4 c3) {
+  if (on & (n >= 16)) lwr16(p, c0);
+  if (on & (n >= 32)) lwr16(p + 16, c1);
+  if (on & (n >= 48)) lwr16(p + 32, c2);
+  if (on & (n >= 64)) lwr16(p + 48, c3);
+  const uint32_t t = n >> 4;
+  const u32x4 ct = t == 0 ? c0 : (t == 1 ? c1 : (t == 2 ? c2 : c3));
+  if (on & ((n & 15u) != 0)) lds_exact(p + 16 * t, ct, n & 15u);
+}
+
+template <uint32_t OUT>
+__global__ __launch_bounds__(64) void op_exec_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    const uint32_t* __restrict__ index, uint32_t n, const uint32_t* __restrict__ count,
+    const uint32_t* __restrict__ rec, const uint2* __restrict__ meta) {
+  using namespace ops;
+  // The output image at its destination's alignment, + 64 bytes so that
+  // 64-byte source reads at any offset stay inside.
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[OUT + 16 + 80];
+  const uint32_t slot = blockIdx.x;
+  if (slot >= (count ? uni(*count) : n)) return;
+  const uint32_t mx = uni(meta[slot].x), want = uni(meta[slot].y);
+  const uint32_t state = mx & 0xc0000000u, nops = mx & 0x3fffffffu;
+  if (state == 0) return;                                  // pass 1 wrote its status
+  const uint32_t i = uni(index ? index[slot] : slot);
+  const uint32_t lane = lane_id();
+  const gptr<uint8_t> dst = to_global(out) + uni64(out_off[i]);
+  uint8_t* const o = s_img + ((uint32_t)reinterpret_cast<uintptr_t>(dst) & 15u);
+  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
+  if (state == kSelf) {
+    const uint32_t slen = uni(in_len[i]);
+    const uint32_t cap = uni(out_cap[i] < OUT ? out_cap[i] : OUT);
+    uint32_t w = 0;
+    const uint32_t st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &w);
+    order();
+    if (st == 1) flush_out(dst, s_img, w);
+    if (lane == 0) {
+      status[i] = (uint8_t)st;
+      out_len[i] = st == 1 ? w : 0;
+    }
+    return;
+  }
+  const gptr<const uint32_t> rp = to_global(rec) + (size_t)slot * kK;
+  uint32_t carry = 0;
+  for (uint32_t b = 0; b < nops; b += kWave) {
+    const bool valid = b + lane < nops;
+    const uint32_t r = valid ? rp[b + lane] : 0u;
+    const bool isc = valid & (r >> 31 != 0);
+    const uint32_t len = valid ? ((r >> 17) & 0x3fffu) + 1 : 0u;
+    const uint32_t x = r & 0x1ffffu;                       // literal: stream offset; copy: distance
+    const uint32_t incl = wave_incl_sum(len);
+    const uint32_t d = carry + incl - len;                 // output offset
+    carry += lane_val(incl, kWave - 1);
+
+    // 1. literals of <= 64 bytes, one per lane: five 16-byte loads in flight
+    //    (clamped to the literal's first piece when past it), then writes.
+    const bool lit = valid & !isc;
+    const bool sl = lit & (len <= 64);
+    {
+      const uint32_t a = sl ? x : 0u, ln = sl ? len : 0u;
+      const u32x4 c0 = ld16(src + a);
+      const u32x4 c1 = ld16(src + a + (ln > 16 ? 16u : 0u));
+      const u32x4 c2 = ld16(src + a + (ln > 32 ? 32u : 0u));
+      const u32x4 c3 = ld16(src + a + (ln > 48 ? 48u : 0u));
+      lds_put64(o + d, len, sl, c0, c1, c2, c3);
+    }
+    // 2. longer literals: the whole wave on one at a time.
+    for (uint64_t big = ballot(lit & (len > 64)); big; big &= big - 1) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(big);
+      const uint32_t bx = lane_val(x, l), bl = lane_val(len, l), bd = lane_val(d, l);
+      for (uint32_t t = 16 * lane; ballot(t < bl); t += 16 * kWave) {
+        const u32x4 v = ld16(src + bx + (t < bl ? t : 0u));
+        if (t + 16 <= bl) lwr16(o + bd + t, v);
+        else if (t < bl) lds_exact(o + bd + t, v, bl - t);
+      }
+    }
+    order();
+    // 3. copies (snappy.c:326-331).  Parallel: those whose source starts at
+    //    or after the end of the batch's previous copy, or ends before its
+    //    first, and does not overlap the copy's own output -- no earlier
+    //    copy of the batch writes a byte they read.
+    const uint32_t pm = wave_shr1(wave_incl_max(isc ? d + len : 0u));
+    const uint64_t cm = ballot(isc);
+    const uint32_t first = cm ? lane_val(d, (uint32_t)__builtin_ctzll(cm)) : 0u;
+    const uint32_t s0 = d - x;
+    const bool indep = isc & (x >= len) & ((s0 >= pm) | (s0 + len <= first));
+    if (ballot(indep)) {
+      const uint32_t a = indep ? s0 : 0u;
+      const u32x4 c0 = lrd16(o + a), c1 = lrd16(o + a + 16), c2 = lrd16(o + a + 32),
+                  c3 = lrd16(o + a + 48);
+      lds_put64(o + d, len, indep, c0, c1, c2, c3);
+    }
+    order();
+    //    The rest in order, a byte per lane (an overlapping copy repeats its
+    //    dist-byte pattern: the reference's forward byte loop).
+    for (uint64_t dm = ballot(isc & !indep); dm; dm &= dm - 1) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(dm);
+      const uint32_t cd = lane_val(d, l), cl = lane_val(len, l), cx = lane_val(x, l);
+      uint32_t from = cd - cx + lane;
+      if (cx < cl) from = cd - cx + lane % cx;
+      if (lane < cl) o[cd + lane] = o[from];
+      order();
+    }
+  }
+  order();
+  flush_out(dst, s_img, want);
+  if (lane == 0) {
+    status[i] = 1;
+    out_len[i] = want;
+  }
+}
+
+hipError_t launch_decode_ops(const DecodeArgs& a, hipStream_t s) {
+  using namespace ops;
+  const size_t rec_bytes = (size_t)a.n * kK * sizeof(uint32_t);
+  Scratch scratch(rec_bytes + (size_t)a.n * sizeof(uint2), s);
+  hipError_t e = scratch.status();
+  if (e != hipSuccess) return e;
+  uint32_t* rec = (uint32_t*)scratch.get();
+  uint2* meta = (uint2*)((uint8_t*)scratch.get() + rec_bytes);
+  hipLaunchKernelGGL((tag_scan_kernel<kBL>), dim3((a.n + kBL - 1) / kBL), dim3(64), 0, s, a.in,
+                     a.in_off, a.in_len, a.out_cap, a.out_len, a.status, a.index, a.n, a.count,
+                     rec, meta);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL((op_exec_kernel<kOut>), dim3(a.n), dim3(64), 0, s, a.in, a.in_off, a.in_len,
+                     a.out, a.out_off, a.out_cap, a.out_len, a.status, a.index, a.n, a.count,
+                     rec, meta);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return scratch.release();
+}
+
 constexpr uint32_t kDecCap0 = 4608;    // fillseq "4 KiB" blocks (max 4208 B)
+static_assert(kDecCap0 == ops::kOut, "the two-pass decoder's class is the 4 KiB class");
 constexpr uint32_t kDecCap1 = 16896;   // 16 KiB class
 constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoot)
 
@@ -2128,7 +2548,9 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
   LGS_TRY(launch_classify(a.out_cap, a.n, kDecCap0, kDecCap1, kDecCap2, list, cnt, s));
   DecodeArgs c = a;
   c.index = list; c.count = cnt;
-  LGS_TRY((a.n >= kLaneMinBlocks ? launch_decode_ring(c, s) : launch_decode_cls<kDecCap0, 1>(c, s)));
+  const int force = options().decoder.load(std::memory_order_relaxed);
+  LGS_TRY((force == kDecOps ? launch_decode_ops(c, s)
+           : a.n >= kLaneMinBlocks ? launch_decode_ring(c, s) : launch_decode_cls<kDecCap0, 1>(c, s)));
   c.index = list + a.n; c.count = cnt + 1;
   LGS_TRY(launch_decode_mid(c, s));
   if (max_out > kDecCap1) {            // (classes above max_out are empty)
@@ -2145,8 +2567,9 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   const int force = options().decoder.load(std::memory_order_relaxed);
-  if (force == kDecAuto && !a.index && max_out > kDecCap0 && a.n >= kSplitMinBlocks &&
-      options().split.load(std::memory_order_relaxed))
+  if (force == kDecOps && max_out <= kDecCap0) return launch_decode_ops(a, s);
+  if ((force == kDecAuto || force == kDecOps) && !a.index && max_out > kDecCap0 &&
+      a.n >= kSplitMinBlocks && options().split.load(std::memory_order_relaxed))
     return launch_decode_split(a, max_out, s);
   if (force == kDecQuad) return launch_decode_quad(a, s);
   if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))

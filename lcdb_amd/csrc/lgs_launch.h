@@ -14,7 +14,7 @@ namespace lgs {
 // Process-wide kernel choices (lgs_set_option; the initial values come from
 // LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
 // launch path reads the environment).
-enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3 };
+enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4 };
 // Outputs over the 16 KiB class: the one-tag walk (default) or the trip
 // decoder (up to 8 tags per step; exact, slower: DESIGN §4.2).
 enum WideKernel { kWideWalk = 0, kWideTrips = 1 };

@@ -197,7 +197,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "ring", "quad"])
+@pytest.mark.parametrize("kernel", ["wave", "ring", "quad", "ops"])
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -224,7 +224,7 @@ def test_decode_kernels_c2_full_size(gpu, digests, force):
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
-    for kernel in ("ring", "wave", "quad"):
+    for kernel in ("ring", "wave", "quad", "ops"):
         force("decoder", kernel)
         out = batch.decode_slots(c.len)
         st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
@@ -291,7 +291,7 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["ring", "quad"])
+@pytest.mark.parametrize("kernel", ["ring", "quad", "ops"])
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
@@ -353,7 +353,72 @@ def _runahead_stream(want: int, copy_frac: float) -> bytes:
     return bytes(s)
 
 
-@pytest.mark.parametrize("kernel", [None, "ring", "quad"])
+def _header(s: bytes):
+    # varint32 of coding.h:169-204 as snappy_decode_size reads it (None: bad)
+    v = 0
+    for k in range(min(5, len(s))):
+        v |= (s[k] & 0x7F) << (7 * k)
+        if not s[k] & 0x80:
+            return v if v <= 0x7FFFFFFF else None
+    return None
+
+
+def test_decode_ops_rejects_overflow_and_jumps(gpu, vectors, force):
+    # The two-pass decoder (ops) on its own class, every outcome against the
+    # reference: the golden compressed streams (corrupt ones included) at a
+    # 4 608-byte capacity; 3 000 corruptions of fillseq blocks (byte flips,
+    # truncations, appended bytes); streams with more ops than pass 1 records
+    # (decoded by pass 2 from the stream alone); long literals that jump the
+    # pass-1 ring past whole segments; the empty block.
+    import random
+    force("decoder", "ops")
+    ref = oracle.best()
+    rng = random.Random(11)
+    cap = 4608
+    streams = [v.a for v in vectors if v.kind == 1]
+    good = [ref.encode(b) for b in corpus.fillseq(1000).blocks()]
+    streams += good
+    for _ in range(3000):
+        s = bytearray(rng.choice(good))
+        r = rng.randrange(4)
+        if r == 0:
+            for _ in range(rng.randrange(1, 4)):
+                s[rng.randrange(len(s))] = rng.randrange(256)
+        elif r == 1:
+            del s[rng.randrange(1, len(s)):]
+        elif r == 2:
+            s += bytes(rng.randrange(256) for _ in range(rng.randrange(1, 6)))
+        else:
+            s[rng.randrange(min(len(s), 6))] ^= 1 << rng.randrange(8)
+        streams.append(bytes(s))
+    # > 1024 ops: 1-byte literals and 4-byte COPY1s (dist 1) alternating
+    many = bytearray(_varint(4600))
+    for _ in range(920):
+        many += bytes([0, 0x61]) + bytes([(0 << 2) | 1, 1])
+    streams += [bytes(many), bytes(many[:-1]), bytes(many[:-3]) + b"\x01\x09"]
+    for _ in range(40):
+        parts = []
+        while sum(map(len, parts)) < 4000:
+            k = rng.randrange(3)
+            n = rng.randrange(1, 700)
+            parts.append(bytes(rng.randrange(256) for _ in range(n)) if k == 0 else
+                         bytes(n) if k == 1 else (b"key%05d" % rng.randrange(99999)) * (n // 8 + 1))
+        raw = b"".join(parts)[:rng.randrange(3000, 4601)]
+        streams.append(ref.encode(raw))
+    streams += [b"\x00", b"", b"\x80", b"\x05\x10abcd"]
+    res, st = gpu.decode_batch_host(streams, [cap] * len(streams))
+    for k, (s, o, code) in enumerate(zip(streams, res, st)):
+        exp = ref.decode(s) if s else None
+        h = _header(s)
+        if exp is not None and len(exp) <= cap:
+            assert code == gpu.LGS_ST_OK and o == exp, k
+        elif h is not None and h > cap:
+            assert code == gpu.LGS_ST_NOSPACE, k
+        else:
+            assert code == gpu.LGS_ST_CORRUPT, k
+
+
+@pytest.mark.parametrize("kernel", [None, "ring", "quad", "ops"])
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
