@@ -109,6 +109,19 @@ __device__ __forceinline__ uint64_t lds_ld64(const uint8_t* base, uint32_t at) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// lds_ld64 in two halves: the three dword reads now, the combine at first
+// use (so the reads' latency can pass under other work in between).
+struct Raw64 {
+  uint32_t a, b, c, s;
+  __device__ uint64_t value() const {
+    return ((uint64_t)__builtin_amdgcn_alignbyte(c, b, s) << 32) | __builtin_amdgcn_alignbyte(b, a, s);
+  }
+};
+__device__ __forceinline__ Raw64 lds_raw64(const uint8_t* base, uint32_t at) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));
+  return Raw64{w[0], w[1], w[2], at & 3u};
+}
+
 // 16 bytes starting at `at` (bytes at..at+15): five aligned dwords.
 __device__ __forceinline__ u32x4 lds_ld128(const uint8_t* base, uint32_t at) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));

@@ -70,6 +70,7 @@ struct LdsIn {
   // (Aligned dwords + v_alignbyte: the same reads as unaligned ds_read_b64 /
   // b32 took C2 encode from 783 to 1 515 us, profiles/r3d_unaligned_lds_ab.txt.)
   __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(x, p); }
+  __device__ Raw64 raw64(uint32_t p) const { return lds_raw64(x, p); }
   __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(x, p); }
   __device__ uint32_t byte(uint32_t p) const { return x[p]; }
   __device__ u32x4 lit128(uint32_t p) const { return lds_ld128(x, p); }
@@ -91,6 +92,7 @@ struct WinIn {
   uint32_t hu;                   // staged below u = hu (a multiple of 16); valid: u >= hu - W
   __device__ uint32_t ri(uint32_t p) const { return (p + sh) & (W - 1); }
   __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(ring, ri(p)); }
+  __device__ Raw64 raw64(uint32_t p) const { return lds_raw64(ring, ri(p)); }
   __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(ring, ri(p)); }
   __device__ uint32_t byte(uint32_t p) const { return ring[ri(p)]; }
   // bytes p .. p+k-1 are not in the ring
@@ -495,13 +497,23 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   // the copy that follows.  (Loops with several exits get a selector
   // variable and compare chains from the compiler's loop-exit unification:
   // scalar work on every trip.)
-  for (;;) {
-    const uint32_t v = kv + lane;
+  // The batch's probe placement from (kv, start) -- its valid lanes and
+  // positions -- and the read of its bytes.  Called for the next batch as
+  // soon as its start is known (right after a copy's extension), so the read
+  // is in flight while this batch records its op and updates the loop state.
+  uint32_t p = 0;
+  bool valid = false, isA = false, isB = false;
+  uint64_t vmask = 0;
+  Raw64 xr = {0, 0, 0, 0};
+  // past: the search has ended (no batch follows; every lane invalid, and
+  // no probe-table load and wait for it).
+  auto place = [&](uint32_t kv_, uint32_t start_, bool past) {
+    const uint32_t v = kv_ + lane;
     uint32_t o0 = e0, o1 = e1;                      // kv == 0: see encode_kernel
-    bool in_tab = true;
-    if (kv != 0) {                                  // other batches: later schedule
+    bool in_tab = !past;
+    if ((kv_ != 0) & !past) {                       // other batches: later schedule
       const uint32_t kk = v - 2;                    // (kv >= 2 here)
-      if (kv + 62 <= kProbeClosed) {                // a chunk's first batch: no load
+      if (kv_ + 62 <= kProbeClosed) {               // a chunk's first batch: no load
         o0 = probe_off(kk);
         o1 = probe_off(kk + 1);
       } else {
@@ -516,13 +528,17 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
         __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
       }
     }
-    const bool isA = v == 0, isB = v == 1;
-    const bool valid = in_tab && start + o1 <= last;              // snappy.c:143
-    const uint64_t vmask = ballot(valid);
-    const uint32_t p = valid ? start + o0 : 0;
-
-    if constexpr (IN::kWin) x.ensure(start + lane_val(o0, 63) + 16);  // lane 63: the last probe
-    uint64_t xw = x.rd64(p);                                      // bytes p .. p+7
+    isA = v == 0;
+    isB = v == 1;
+    valid = in_tab && start_ + o1 <= last;                        // snappy.c:143
+    vmask = ballot(valid);
+    p = valid ? start_ + o0 : 0;
+    if constexpr (IN::kWin) x.ensure(start_ + lane_val(o0, 63) + 16);  // lane 63: the last probe
+    xr = x.raw64(p);                                              // bytes p .. p+7
+  };
+  place(kv, start, false);
+  for (;;) {
+    uint64_t xw = xr.value();
     if constexpr (IN::kWin) {
       const bool op_ = valid & x.oow(p, 8);
       if (ballot(op_)) xw = op_ ? x.g64(p) : xw;
@@ -565,6 +581,7 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     // loop state with selects (one set of loop-carried values, no per-path
     // copies of them at the latch).
     uint32_t at_n = at;
+    bool done;
     if (mm) {
       const uint32_t m = (uint32_t)__builtin_ctzll(mm);           // the matching probe
       const uint32_t base = lane_val(p, m);
@@ -599,6 +616,9 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
         at_n += kWave;
         r += kWave;
       }
+      // Match: the search restarts after the copy (snappy.c:169, 184-185).
+      done = at_n >= last;
+      place(0u, at_n + 1, false);       // (also when done: harmless, and no copies at the latch)
 
       // snappy.c:156 + 166: the literal before the copy (empty after a
       // re-match), then the copy -- recorded, emitted by flush_ops.
@@ -609,11 +629,12 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
         nops = 0;
         lit0 = at_n;
       }
+    } else {
+      // No match: the search ends if a probe of the batch was past the limit
+      // (snappy.c:143), else continues with the next 64 probes.
+      done = vmask != ~0ull;
+      place(kv + kWave, start, done);
     }
-    // Match: the search restarts after the copy (snappy.c:169, 184-185).
-    // No match: it ends if a probe of the batch was past the limit
-    // (snappy.c:143), else continues with the next 64 probes.
-    const bool done = mm ? at_n >= last : vmask != ~0ull;
     lit = mm ? at_n : lit;
     start = mm ? at_n + 1 : start;
     kv = mm ? 0u : kv + kWave;
