@@ -597,8 +597,11 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
       for (;;) {                                                  // snappy.c:163-164
         const uint32_t q = at_n + lane;
         if constexpr (IN::kWin) x.ensure(at_n + kWave);
-        // Clamped unconditional reads (q < n implies r + lane < n).
-        const uint32_t qa = q < n ? q : 0, ra = q < n ? r + lane : 0;
+        // Unconditional reads, unclamped: lanes at q >= n read at most 63
+        // bytes past the chunk (the LDS image has that slack; the window
+        // ring masks its index) and their bytes are discarded by `same`.
+        // (r + lane < q: the source starts before the copy.)
+        const uint32_t qa = q, ra = r + lane;
         uint32_t br = x.byte(ra), bq = x.byte(qa);
         if constexpr (IN::kWin) {
           const bool orq = (q < n) & (x.oow(ra, 1) || x.oow(qa, 1));
@@ -688,7 +691,10 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
     const uint32_t* __restrict__ count) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 48];
+  // + 48: the staging shift and zero pad; + 64: the match extension's reads
+  // past the chunk (encode_chunk).  8 832 B with the table: still 18 waves
+  // per CU (the 1 280-byte LDS granule).
+  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 112];
   __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap + 8];   // + sink
 
   // Per-wave scalars go through v_readfirstlane so hipcc keeps the control
