@@ -131,6 +131,36 @@ __device__ __forceinline__ u32x4 lds_ld128(const uint8_t* base, uint32_t at) {
                __builtin_amdgcn_alignbyte(d, c, s), __builtin_amdgcn_alignbyte(e, d, s)};
 }
 
+// Copy `len` bytes global->LDS with byte k of the source at lds[k] (lds
+// 16-byte aligned), so dword reads of the image are aligned whatever the
+// source's alignment.  The global reads are 16 bytes per lane at any byte
+// address and may touch up to 15 bytes past the end (the callers' read
+// slack); one zero granule is written past the image.  Up to R loads per
+// lane are in flight before the first LDS write, so a 4 KiB block (257
+// granules, R = 5) costs one memory round trip, not one per 1 KiB.
+template <uint32_t R>
+__device__ __forceinline__ void stage_in_linear(uint8_t* lds, gptr<const uint8_t> src,
+                                                uint32_t len) {
+  typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
+  u32x4* l = reinterpret_cast<u32x4*>(lds);
+  const uint32_t n16 = (len + 15u) >> 4, lane = lane_id();
+#pragma clang loop unroll(disable)
+  for (uint32_t c0 = 0; c0 < n16; c0 += R * kWave) {
+    u32x4 v[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const uint32_t c = c0 + k * kWave + lane;
+      v[k] = *(gptr<const u32x4_a1>)(src + 16 * (c < n16 ? c : 0u));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const uint32_t c = c0 + k * kWave + lane;
+      if (c < n16) l[c] = v[k];
+    }
+  }
+  if (lane == 0) l[n16] = u32x4{0, 0, 0, 0};
+}
+
 // Copy `len` bytes global->LDS: the LDS image keeps the source's alignment
 // mod 16 (byte k of the source lands at lds[(src & 15) + k]) so that every
 // lane moves one aligned 16-byte granule.  Returns the LDS shift (src & 15).

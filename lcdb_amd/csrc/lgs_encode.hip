@@ -691,7 +691,7 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
     const uint32_t* __restrict__ count) {
-  // + 48: the staging shift and zero pad; + 64: the match extension's reads
+  // + 48: the zero granule past the image (and spare); + 64: the match extension's reads
   // past the chunk (encode_chunk).  8 832 B with the table: still 18 waves
   // per CU (the 1 280-byte LDS granule).
   __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 112];
@@ -722,8 +722,12 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   // (IN_CAP >= min(len, 65536) is guaranteed by the launcher.)
   for (uint32_t c0 = 0; c0 < len; c0 += kChunk) {
     const uint32_t clen = len - c0 < kChunk ? len - c0 : kChunk;
-    const uint32_t sh = stage_in(&s_in[wv][0], src + c0, clen);
-    LdsIn x{&s_in[wv][sh]};
+    // Byte k of the chunk at s_in[k]: the image's dword reads are aligned
+    // for any input alignment (unaligned LDS dword reads took C2 encode from
+    // 0.78 to 1.5 ms, see LdsIn).
+    constexpr uint32_t kR = (IN_CAP + 16 + 1023) / 1024 < 8 ? (IN_CAP + 16 + 1023) / 1024 : 8;
+    stage_in_linear<kR>(&s_in[wv][0], src + c0, clen);
+    LdsIn x{&s_in[wv][0]};
     order();
     if (clen >= kMinBlock) {
       op = encode_chunk(x, clen, &s_tab[wv][0], o, op, e0, e1);

@@ -28,6 +28,11 @@ def child(lib: str) -> None:
     import torch
     from lcdb_amd import batch, corpus
     c = corpus.fillseq(65536)
+    k = int(os.environ.get("PROBE_SHIFT", "0"))
+    if k:   # every block k bytes off its 16-byte alignment
+        buf = np.zeros(len(c.buf) + k, dtype=np.uint8)
+        buf[k:] = c.buf
+        c = corpus.Corpus(buf, c.off + np.uint64(k), c.len)
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     out = batch.decode_slots(c.len)
