@@ -459,7 +459,8 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   uint32_t want = 0, st = 3;
   if (slen <= kBuf - 48 - 256) {
     const uint32_t ib = (kBuf - slen - 48 - 256) & ~15u;
-    const uint32_t sh = stage_in(&s_buf[wv][ib], src, slen);
+    constexpr uint32_t kR = (kBuf + 1023) / 1024 < 8 ? (kBuf + 1023) / 1024 : 8;
+    const uint32_t sh = stage_in<kR>(&s_buf[wv][ib], src, slen);
     order();
     st = decode_win(&s_buf[wv][ib], sh, slen, o, (int32_t)ib - (int32_t)oshift, cap, &want);
     order();

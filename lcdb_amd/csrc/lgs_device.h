@@ -165,15 +165,30 @@ __device__ __forceinline__ void stage_in_linear(uint8_t* lds, gptr<const uint8_t
 // mod 16 (byte k of the source lands at lds[(src & 15) + k]) so that every
 // lane moves one aligned 16-byte granule.  Returns the LDS shift (src & 15).
 // Reads may touch the aligned 16-byte granules that contain the first and
-// last byte, never a different page.
+// last byte, never a different page.  Up to R granules per lane are in
+// flight before the first LDS write (one memory round trip per R KiB).
+template <uint32_t R = 1>
 __device__ __forceinline__ uint32_t stage_in(uint8_t* lds, gptr<const uint8_t> src, uint32_t len) {
   const uint32_t shift = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 15u);
   gptr<const u32x4> g = (gptr<const u32x4>)(src - shift);
   u32x4* l = reinterpret_cast<u32x4*>(lds);
-  const uint32_t n16 = (shift + len + 15u) >> 4;
-  for (uint32_t c = lane_id(); c < n16; c += kWave) l[c] = g[c];
+  const uint32_t n16 = (shift + len + 15u) >> 4, lane = lane_id();
+#pragma clang loop unroll(disable)
+  for (uint32_t c0 = 0; c0 < n16; c0 += R * kWave) {
+    u32x4 v[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const uint32_t c = c0 + k * kWave + lane;
+      v[k] = g[c < n16 ? c : 0u];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const uint32_t c = c0 + k * kWave + lane;
+      if (c < n16) l[c] = v[k];
+    }
+  }
   // Zero pad one granule past the end so fixed-width window reads are defined.
-  if (lane_id() == 0) l[n16] = u32x4{0, 0, 0, 0};
+  if (lane == 0) l[n16] = u32x4{0, 0, 0, 0};
   return shift;
 }
 

@@ -36,6 +36,11 @@ def child(lib: str) -> None:
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     out = batch.decode_slots(c.len)
+    kd = int(os.environ.get("PROBE_DSHIFT", "0"))
+    if kd:  # compressed streams and outputs kd bytes off their 16-byte alignment
+        comp.off += kd
+        out = batch.decode_slots(c.len + 16)
+        out.off += kd
     st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
     res = {"lib": os.path.basename(lib) + (("@" + os.environ["LGS_DECODE_KERNEL"])
