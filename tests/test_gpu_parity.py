@@ -256,6 +256,38 @@ def test_encode_small_batch_and_c1(gpu, vectors, digests):
     assert batch.digest(comp) == (d["comp_sha256"], d["comp_bytes"]), kernel
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3, 7, 13])
+def test_misaligned_blocks_c1_round_trip(gpu, digests, force, shift):
+    # Every block (input, compressed stream and output) `shift` bytes off its
+    # 16-byte alignment: the encoder's linear staging (16-byte loads at any
+    # address) and every decoder's handling of odd stream and output offsets
+    # against the pinned C1 digests; the ring decoder forced (C1 is below its
+    # batch threshold), then the default wave decoder.
+    import torch
+    from lcdb_amd import batch
+    d = digests["C1_fillseq_1024x4KiB"]
+    c = corpus.fillseq(1024)
+    buf = np.zeros(len(c.buf) + shift, dtype=np.uint8)
+    buf[shift:] = c.buf
+    cs = corpus.Corpus(buf, c.off + np.uint64(shift), c.len)
+    raw = batch.upload(cs)
+    comp = batch.encode_slots(raw)
+    comp.off += shift
+    batch.encode(raw, comp)
+    hc = batch.to_host(comp)
+    assert corpus.digest_of_digests(corpus.block_digests(hc.buf, hc.off, hc.len)) == d["comp_dd"]
+    for kernel in ("ring", "auto"):
+        force("decoder", kernel)
+        out = batch.decode_slots(c.len + 16)
+        out.off += shift
+        st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
+        batch.decode(comp, out, st)
+        torch.cuda.synchronize()
+        assert bool((st == 1).all()), kernel
+        ho = batch.to_host(out)
+        assert corpus.digest_of_digests(corpus.block_digests(ho.buf, ho.off, ho.len)) == d["raw_dd"]
+
+
 def test_encode_c2_and_random(gpu, digests):
     # The encoder on the full C2 corpus, then on random, zero, periodic and
     # short inputs of every length class in one batch.
