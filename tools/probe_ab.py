@@ -37,10 +37,13 @@ def child(lib: str) -> None:
     comp = batch.encode_slots(raw)
     out = batch.decode_slots(c.len)
     kd = int(os.environ.get("PROBE_DSHIFT", "0"))
-    if kd:  # compressed streams and outputs kd bytes off their 16-byte alignment
-        comp.off += kd
+    kc = int(os.environ.get("PROBE_CSHIFT", str(kd)))   # compressed streams only
+    ko = int(os.environ.get("PROBE_OSHIFT", str(kd)))   # decoder outputs only
+    if kc:  # compressed streams kc bytes off their 16-byte alignment
+        comp.off += kc
+    if ko:  # decoder outputs ko bytes off
         out = batch.decode_slots(c.len + 16)
-        out.off += kd
+        out.off += ko
     st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
     res = {"lib": os.path.basename(lib) + (("@" + os.environ["LGS_DECODE_KERNEL"])
