@@ -598,8 +598,8 @@ int host_verdict(uint32_t want, size_t m) {
 // Device memory for an over-slot decode.  A valid stream must never come
 // back as corrupt because memory is short for a moment (lcdb
 // would turn that 0 into a lasting LDB_CORRUPTION background error), so a
-// failed hipMalloc is retried with a growing back-off (about 2 s in all)
-// before the call fails -- and then ldb_snappy_decode aborts with a
+// failed hipMalloc is tried 13 times, 12 sleeps from 0.5 ms doubling to a
+// 256 ms cap between them (about 1 s in all), before the call fails -- and then ldb_snappy_decode aborts with a
 // diagnostic, as on any other device failure.  Test hook:
 // lgs_set_option("inject_alloc_failures", "N") makes the next N attempts
 // fail as if the device were out of memory.

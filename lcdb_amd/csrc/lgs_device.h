@@ -110,16 +110,26 @@ __device__ __forceinline__ uint64_t lds_ld64(const uint8_t* base, uint32_t at) {
 }
 
 // lds_ld64 in two halves: the three dword reads now, the combine at first
-// use (so the reads' latency can pass under other work in between).
+// use (so the reads' latency can pass under other work in between).  `s` is
+// the unmasked byte address: v_alignbyte_b32 reads only its low two bits.
 struct Raw64 {
   uint32_t a, b, c, s;
-  __device__ uint64_t value() const {
-    return ((uint64_t)__builtin_amdgcn_alignbyte(c, b, s) << 32) | __builtin_amdgcn_alignbyte(b, a, s);
-  }
+  __device__ uint32_t lo() const { return __builtin_amdgcn_alignbyte(b, a, s); }
+  __device__ uint32_t hi() const { return __builtin_amdgcn_alignbyte(c, b, s); }
+  __device__ uint64_t value() const { return ((uint64_t)hi() << 32) | lo(); }
 };
 __device__ __forceinline__ Raw64 lds_raw64(const uint8_t* base, uint32_t at) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));
-  return Raw64{w[0], w[1], w[2], at & 3u};
+  return Raw64{w[0], w[1], w[2], at};
+}
+// The same for lds_ld32: two dword reads now, the combine at first use.
+struct Raw32 {
+  uint32_t a, b, s;
+  __device__ uint32_t value() const { return __builtin_amdgcn_alignbyte(b, a, s); }
+};
+__device__ __forceinline__ Raw32 lds_raw32(const uint8_t* base, uint32_t at) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (at & ~3u));
+  return Raw32{w[0], w[1], at};
 }
 
 // 16 bytes starting at `at` (bytes at..at+15): five aligned dwords.
@@ -134,17 +144,22 @@ __device__ __forceinline__ u32x4 lds_ld128(const uint8_t* base, uint32_t at) {
 // Copy `len` bytes global->LDS with byte k of the source at lds[k] (lds
 // 16-byte aligned), so dword reads of the image are aligned whatever the
 // source's alignment.  The global reads are 16 bytes per lane at any byte
-// address and may touch up to 15 bytes past the end (the callers' read
-// slack); one zero granule is written past the image.  Up to R loads per
-// lane are in flight before the first LDS write, so a 4 KiB block (257
-// granules, R = 5) costs one memory round trip, not one per 1 KiB.
+// address, all inside [src, src + len): a ragged last granule is read as
+// the 16 bytes that end at src + len and shifted into place (a block that
+// ends flush with the end of a page or allocation must not fault), and a
+// block under 16 bytes is read a byte per lane.  The image's bytes past len
+// in its last granule are zero, and one zero granule is written past it.
+// Up to R loads per lane are in flight before the first LDS write, so a
+// 4 KiB block (257 granules, R = 5) costs one memory round trip, not one
+// per 1 KiB.
 template <uint32_t R>
 __device__ __forceinline__ void stage_in_linear(uint8_t* lds, gptr<const uint8_t> src,
                                                 uint32_t len) {
   typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
   u32x4* l = reinterpret_cast<u32x4*>(lds);
   const uint32_t n16 = (len + 15u) >> 4, lane = lane_id();
-#pragma clang loop unroll(disable)
+#ifdef LGS_PROBE_OLD_STAGE
+  // Probe build: round 3's staging (reads up to 15 bytes past the block).
   for (uint32_t c0 = 0; c0 < n16; c0 += R * kWave) {
     u32x4 v[R];
 #pragma unroll
@@ -157,6 +172,47 @@ __device__ __forceinline__ void stage_in_linear(uint8_t* lds, gptr<const uint8_t
       const uint32_t c = c0 + k * kWave + lane;
       if (c < n16) l[c] = v[k];
     }
+  }
+  if (lane == 0) l[n16] = u32x4{0, 0, 0, 0};
+  return;
+#endif
+  if (len < 16) {                                   // one ragged granule, no full one
+    if (lane < 16) lds[lane] = lane < len ? src[lane] : (uint8_t)0;
+    if (lane == 0) l[1] = u32x4{0, 0, 0, 0};
+    return;
+  }
+  // The whole granules, then (d != 0) the ragged last one, nfull, read as
+  // the 16 bytes that end at src + len by lane 0, its load issued first.
+  const uint32_t nfull = len >> 4, d = (16u - (len & 15u)) & 15u;
+  u32x4 tail = u32x4{0, 0, 0, 0};
+  if ((d != 0) & (lane == 0)) tail = *(gptr<const u32x4_a1>)(src + (len - 16));
+#pragma clang loop unroll(disable)
+  for (uint32_t c0 = 0; c0 < nfull; c0 += R * kWave) {
+    u32x4 v[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const uint32_t c = c0 + k * kWave + lane;
+      v[k] = *(gptr<const u32x4_a1>)(src + 16 * (c < nfull ? c : 0u));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const uint32_t c = c0 + k * kWave + lane;
+      if (c < nfull) l[c] = v[k];
+    }
+  }
+  if ((d != 0) & (lane == 0)) {
+    // Shift it down by d bytes, zeros in: word i of the granule is bytes
+    // 4i + d .. 4i + d + 3 of the loaded 16.
+    const uint32_t w[8] = {tail.x, tail.y, tail.z, tail.w, 0, 0, 0, 0};
+    const uint32_t q = d >> 2, r = d & 3u;
+    uint32_t o[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint32_t lo = q == 0 ? w[i] : q == 1 ? w[i + 1] : q == 2 ? w[i + 2] : w[i + 3];
+      const uint32_t hi = q == 0 ? w[i + 1] : q == 1 ? w[i + 2] : q == 2 ? w[i + 3] : w[i + 4];
+      o[i] = __builtin_amdgcn_alignbyte(hi, lo, r);
+    }
+    l[nfull] = u32x4{o[0], o[1], o[2], o[3]};
   }
   if (lane == 0) l[n16] = u32x4{0, 0, 0, 0};
 }

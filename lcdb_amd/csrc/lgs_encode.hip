@@ -71,7 +71,7 @@ struct LdsIn {
   // b32 took C2 encode from 783 to 1 515 us, profiles/r3d_unaligned_lds_ab.txt.)
   __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(x, p); }
   __device__ Raw64 raw64(uint32_t p) const { return lds_raw64(x, p); }
-  __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(x, p); }
+  __device__ Raw32 raw32(uint32_t p) const { return lds_raw32(x, p); }
   __device__ uint32_t byte(uint32_t p) const { return x[p]; }
   __device__ u32x4 lit128(uint32_t p) const { return lds_ld128(x, p); }
   __device__ uint32_t litbyte(uint32_t p) const { return x[p]; }
@@ -93,7 +93,7 @@ struct WinIn {
   __device__ uint32_t ri(uint32_t p) const { return (p + sh) & (W - 1); }
   __device__ uint64_t rd64(uint32_t p) const { return lds_ld64(ring, ri(p)); }
   __device__ Raw64 raw64(uint32_t p) const { return lds_raw64(ring, ri(p)); }
-  __device__ uint32_t rd32(uint32_t p) const { return lds_ld32(ring, ri(p)); }
+  __device__ Raw32 raw32(uint32_t p) const { return lds_raw32(ring, ri(p)); }
   __device__ uint32_t byte(uint32_t p) const { return ring[ri(p)]; }
   // bytes p .. p+k-1 are not in the ring
   __device__ bool oow(uint32_t p, uint32_t k) const {
@@ -273,7 +273,7 @@ __device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uin
 }
 
 // The recorded ops of one chunk, emitted lane-parallel: lane k holds op k
-// (recA = copy start << 16 | copy length, recB = copy distance), each op
+// (recA = copy end << 16 | copy start, recB = the copy's source), each op
 // being the literal from the previous op's end (lit0 for op 0) to its copy
 // start, then the copy (snappy.c:156, :166).  Every lane sizes its op
 // (snappy.c:53-102), a wave scan places it, then
@@ -287,17 +287,11 @@ __device__ __forceinline__ uint32_t emit_copy(const OutSlot& o, uint32_t op, uin
 // Returns the output cursor after the k ops.
 constexpr uint32_t kLongLit = 256;
 
-// v_writelane: lane l of a = sa and of b = sb (uniform values and lane).
-// The lane select goes through M0 (gfx950 VALU reads at most one SGPR per
-// instruction); M0 is compiler-reserved, so it is saved and restored inside
-// the statement.
-__device__ __forceinline__ void write_lane2(uint32_t& a, uint32_t sa, uint32_t& b, uint32_t sb,
-                                            uint32_t l) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %2, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
-      "v_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0\n\ts_mov_b32 m0, %2"
-      : "+v"(a), "+v"(b), "=&s"(keep) : "s"(sa), "s"(sb), "s"(l));
+// r = v in the lanes whose bit of the SGPR mask sel is set (one lane: the
+// op's record slot).  A plain v_cndmask with the mask as its condition; in
+// C++ the per-lane bit of an SGPR mask costs a shift and a compare.
+__device__ __forceinline__ void rec_lane(uint32_t& r, uint32_t v, uint64_t sel) {
+  asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(r) : "v"(v), "s"(sel));
 }
 template <class IN>
 __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, const IN& x,
@@ -305,7 +299,9 @@ __device__ __forceinline__ uint32_t flush_ops(const OutSlot& o, uint32_t op, con
                                               uint32_t lit0) {
   const uint32_t lane = lane_id();
   const bool live = lane < k;
-  const uint32_t base = recA >> 16, clen = recA & 0xffffu, dist = recB;
+  // (The copy's end is kept mod 2^16: it is 65 536 when a copy ends a 64 KiB
+  // chunk; the length, at most 65 535, is exact mod 2^16.)
+  const uint32_t base = recA & 0xffffu, clen = ((recA >> 16) - base) & 0xffffu, dist = base - recB;
   const uint32_t pend = (uint32_t)__shfl_up((int)(base + clen), 1);
   const uint32_t lit = lane == 0 ? lit0 : pend;
   const uint32_t LL = live ? base - lit : 0u;
@@ -406,10 +402,11 @@ constexpr bool probe_off_matches_table() {
 }
 static_assert(probe_off_matches_table(), "closed-form probe schedule != snappy.c:138-143");
 
-// Index of the scratch slot every table carries past its 2048 real entries:
-// lanes that must not touch a real entry aim their table access there
-// instead of branching around it (keeps the batch free of exec-mask regions,
-// whose save/branch/restore is scalar work).
+// The table (2 048 u16 entries + a sink) sits at the start of the wave's
+// LDS, the chunk image right after it (EncLds below).  Lanes that must not
+// touch a real entry aim their table access at the sink dword instead of
+// branching around it (keeps the batch free of exec-mask regions, whose
+// save/branch/restore is scalar work).
 constexpr uint32_t kSink = kTableCap;
 
 // LDS address (32-bit, address space 3) of a __shared__ pointer.
@@ -417,20 +414,47 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
 }
 
-// tab[h] = v, returning the entry's previous value, as one LDS atomic on the
-// dword holding the u16 entry (ds_mskor_rtn_b32: mem = (mem & ~mask) | data).
-// The lanes of one such instruction that hit the same dword are applied in
-// ascending lane order, each seeing its predecessors' writes (measured on
-// gfx950, tools/lds_atomic_probe.hip; encode_chunk verifies it per batch).
-__device__ __forceinline__ uint32_t tab_swap(uint16_t* tab, uint32_t h, uint32_t v) {
-  const uint32_t sh = (h & 1u) * 16u;
+// One LDS atomic on the table dword at byte offset a (the table itself at
+// LDS offset TAB, folded into the instruction): mem = (mem & ~mask) | data,
+// returning the old dword.  The lanes of one such instruction that hit the
+// same dword are applied in ascending lane order, each seeing its
+// predecessors' writes (measured on gfx950, tools/lds_atomic_probe.hip;
+// encode_chunk verifies it per batch).
+template <uint32_t TAB>
+__device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t a, uint32_t mask, uint32_t data) {
   uint32_t old;
-  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
-               : "=v"(old)
-               : "v"(lds_addr(tab) + (h >> 1) * 4u), "v"(0xffffu << sh), "v"(v << sh)
-               : "memory");
-  return (old >> sh) & 0xffffu;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(old) : "v"(a), "v"(mask), "v"(data), "i"(TAB) : "memory");
+  return old;
 }
+// The same without the result (and without a wait: LDS operations of one
+// wave execute in issue order).
+template <uint32_t TAB>
+__device__ __forceinline__ void lds_mskor(uint32_t a, uint32_t mask, uint32_t data) {
+  asm volatile("ds_mskor_b32 %0, %1, %2 offset:%3" : : "v"(a), "v"(mask), "v"(data), "i"(TAB)
+               : "memory");
+}
+
+// Per-lane constants of a batch.  Every batch has lanes 0 and 1 reserved
+// for the re-probe that follows a copy (snappy.c:172-186): lane 0 is its A
+// at at - 1, lane 1 its B at at; lanes l >= 2 are search probes k + l - 2 of
+// the literal search (snappy.c:138-143), 62 per batch.  A chunk's first
+// batch and a search's later batches leave lanes 0 and 1 off.  e0: offset of
+// lane l's probe from the search start at + 1 in the batch after a copy; e1:
+// offset of the probe after it (the bound check of snappy.c:143; A and B
+// always pass it: the batch runs only while at < last); bm: 0xffffff in B's
+// lane (its 64-bit compare, snappy.c:182), else 0.
+struct PostLanes {
+  uint32_t e0, e1, bm;
+};
+constexpr uint32_t kProbesPerBatch = kWave - 2;
+__device__ __forceinline__ PostLanes post_lanes(uint32_t lane) {
+  const uint32_t pk = lane >= 2 ? lane - 2 : 0;
+  return PostLanes{lane == 0 ? 0xfffffffeu : (lane == 1 ? 0xffffffffu : probe_off(pk)),
+                   lane < 2 ? 0u : probe_off(pk + 1), lane == 1 ? 0xffffffu : 0u};
+}
+// Offset of the last lane's probe in the first batch of a search (WinIn staging).
+constexpr uint32_t kPostLast = probe_off(kProbesPerBatch - 1);
 
 // Encode one chunk x[0..n), 17 <= n <= 65536, held in LDS.  `tab` is the
 // u16 hash table (with a sink slot).  Writes to o, returns bytes written.
@@ -438,28 +462,46 @@ __device__ __forceinline__ uint32_t tab_swap(uint16_t* tab, uint32_t h, uint32_t
 //
 // Literal-search batches.  Lane l takes the batch's probe l (lane 0 the
 // earliest).  Each valid lane swaps its probe position into tab[hash] with
-// one LDS atomic (tab_swap).  Because a wave's atomics on one address apply
-// in lane order, every lane gets back exactly what snappy.c:146-148 would
-// read at that probe -- the position of the batch's latest earlier probe
-// with the same hash, else the entry as the batch found it -- and the table
-// ends as the serial loop would leave it after all 64 probes.  No lane-id
-// rounds and no cut: any number of probes may share a hash.  The first lane
-// whose 4-byte compare matches ends the search; the probes after it must not
-// have written, so in each slot they touched the first of them restores the
-// value it received (its received value is a committed position or an old
-// entry exactly when it is at most the match's position: positions grow
-// with the lane, old entries lie before the batch).  A lane receiving a
+// one LDS atomic (lds_mskor_rtn on the entry's dword).  Because a wave's
+// atomics on one address apply in lane order, every lane gets back exactly
+// what snappy.c:146-148 would read at that probe -- the position of the
+// batch's latest earlier probe with the same hash, else the entry as the
+// batch found it -- and the table ends as the serial loop would leave it
+// after all 64 probes.  Any number of probes may share a hash.  The first
+// lane whose 4-byte compare matches ends the search; the probes after it
+// must not have written, so in each slot they touched the first of them
+// restores the value it received (its received value is a committed position
+// or an old entry exactly when it is at most the match's position: positions
+// grow with the lane, old entries lie before the batch).  A lane receiving a
 // position later than its own would mean the order assumption broke; then
 // the batch restores the table and replays the swaps one lane at a time.
 //
-// A found match is extended; lcdb's immediate re-probe (snappy.c:172-186)
-// is folded into the next batch (below).  The literal + copy is not emitted
-// on the spot: the op is recorded in lane registers (v_writelane) and 64 ops
-// at a time are emitted lane-parallel (flush_ops), a few VALU per op instead
-// of one 64-lane pass.  (The per-op pass measured 176 against 213 GiB/s.)
-template <class IN>
+// The re-probe after a copy (PostLanes) is two ordinary probes to the table
+// swap, which gives the serial order's table semantics (B's candidate is
+// at-1 when A and B share a hash); A never matches, and B's match is the
+// re-match of snappy.c:182.  Folding the re-probe into the batch removes its
+// three dependent LDS round trips from every copy.
+//
+// A found match is extended and recorded: lane k of recA/recB holds op k,
+// and 64 ops at a time are emitted lane-parallel (flush_ops), a few VALU per
+// op instead of one 64-lane pass.  (The per-op pass measured 176 against
+// 213 GiB/s.)
+//
+// Round 4: the hot path is one loop with one exit -- batch, match,
+// extension, record, the batch after the copy -- and a batch without a
+// match leaves it, to the outer loop that places a search's later batches
+// from the probe table.  The batch after the chunk's last copy runs with
+// every lane off, so the end of the chunk is that same exit.  Every batch
+// has the same lane layout, so B's mask and the lanes that may match need
+// no per-batch state, and validity is computed per batch, not carried.
+// Table addresses come straight from the hash (the image at LDS 0,
+// the table at a constant offset folded into the instruction), and an op is
+// recorded by a one-hot lane mask (rec_lane) instead of v_writelane
+// through M0.
+template <uint32_t TAB, class IN>
 __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* tab,
-                                 const OutSlot& o, uint32_t op0, uint32_t e0, uint32_t e1) {
+                                                 const OutSlot& o, uint32_t op0,
+                                                 const PostLanes& pl) {
   const uint32_t lane = lane_id();
   const uint32_t last = n - kMargin;                  // snappy.c:106
 
@@ -473,192 +515,173 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   for (uint32_t e = lane; e < tsize / 8; e += kWave)
     reinterpret_cast<u32x4*>(tab)[e] = u32x4{0, 0, 0, 0};
   order();
+  // h2 = (x * kHashMul) >> (shift - 1) = 2 * hash32(x, shift) + one more bit:
+  // the entry's dword is at TAB + (h2 & ~3) and its half of that dword is
+  // (h2 & 2) << 3.  (TAB, the table's LDS offset, goes into the instruction.)
+  const uint32_t hsh = shift - 1;
+  constexpr uint32_t kSinkOff = 2 * kSink;            // the sink dword, from the table
 
   uint32_t op = op0;     // output cursor (byte offset in the slot)
-  uint32_t lit = 0;      // first byte not yet emitted (snappy.c:111 "emit")
-  uint32_t at = 0;       // end of the last copy
+  uint32_t at = 0;       // end of the last copy (snappy.c:167 "emit")
   uint32_t start = 1;    // first probe position of the current search (snappy.c:112)
-  uint32_t kv = 2;       // virtual probe index of this batch's lane 0
-  // Recorded ops (lane k = op k), their count, op 0's literal start.
-  uint32_t recA = 0, recB = 0, nops = 0, lit0 = 0;
+  uint32_t kb = 0;       // the search's probe index in lane 2 of the batch
+  uint32_t recA = 0, recB = 0, lit0 = 0;
+  uint64_t sel = 1;      // one-hot: the lane that records the next op
 
-  // Each batch takes 64 consecutive probes of a virtual sequence:
-  //   v = 0: A, position at-1 -- the re-probe's first insert (snappy.c:172-175),
-  //   v = 1: B, position at   -- its insert and 64-bit compare (snappy.c:177-182),
-  //   v >= 2: search probe v-2 from start = at+1 (snappy.c:133-154).
-  // A and B exist only after a copy (a chunk's first search starts at
-  // v = 2).  They are ordinary probes to the table swap, which gives the
-  // serial order's table semantics (B's candidate is at-1 when A and B
-  // share a hash); A never matches, and B's match is the re-match of
-  // snappy.c:182.  Folding the re-probe into the batch removes its three
-  // dependent LDS round trips from every copy.
-  //
-  // One loop with one exit: each trip is one batch and, if it finds a match,
-  // the copy that follows.  (Loops with several exits get a selector
-  // variable and compare chains from the compiler's loop-exit unification:
-  // scalar work on every trip.)
-  // The batch's probe placement from (kv, start) -- its valid lanes and
-  // positions -- and the read of its bytes.  Called for the next batch as
-  // soon as its start is known (right after a copy's extension), so the read
-  // is in flight while this batch records its op and updates the loop state.
-  uint32_t p = 0;
-  bool valid = false, isA = false, isB = false;
+  // The batch in flight: each lane's probe position, the lanes that are
+  // probes (vmask), and the read of bytes p .. p+7 (issued when the batch
+  // is placed, combined at first use).
+  uint32_t p;
   uint64_t vmask = 0;
-  Raw64 xr = {0, 0, 0, 0};
-  // past: the search has ended (no batch follows; every lane invalid, and
-  // no probe-table load and wait for it).
-  auto place = [&](uint32_t kv_, uint32_t start_, bool past) {
-    const uint32_t v = kv_ + lane;
-    uint32_t o0 = e0, o1 = e1;                      // kv == 0: see encode_kernel
-    bool in_tab = !past;
-    if ((kv_ != 0) & !past) {                       // other batches: later schedule
-      const uint32_t kk = v - 2;                    // (kv >= 2 here)
-      if (kv_ + 62 <= kProbeClosed) {               // a chunk's first batch: no load
-        o0 = probe_off(kk);
-        o1 = probe_off(kk + 1);
-      } else {
-        in_tab = kk < kProbeTab;
-        const uint32_t kc = in_tab ? kk : kProbeTab - 1;
-        o0 = kProbe.off[kc];
-        o1 = kProbe.off[kc + 1];
-        // Wait for these two loads here, on the rare path.  Left to the
-        // compiler, the wait lands where the paths merge as vmcnt(0) -- and
-        // vmcnt also counts the output stores, so every batch would stall
-        // until the previous copy's bytes had reached memory.
-        __builtin_amdgcn_s_waitcnt(0x0f70);                       // vmcnt(0)
+  Raw64 xr;
+  // The batch's table state, kept for the copy that follows a match.
+  uint32_t prev = 0, h2 = 0, ta = 0, sh = 0, mask = 0;
+  // ---- one batch: snappy.c:146-152 for its 64 probes, `valid` the lanes
+  // that are probes.  Returns the lanes that match.  (Validity is passed in,
+  // not kept: a bool carried around the loop becomes a lane-mask phi merged
+  // with exec on every path.)
+  auto batch = [&](bool valid) -> uint64_t {
+    vmask = ballot(valid);
+    uint32_t xv = xr.lo(), xh = xr.hi();
+    if constexpr (IN::kWin) {
+      const bool o8 = valid & x.oow(p, 8);
+      if (ballot(o8)) {
+        const uint64_t g = x.g64(p);
+        xv = o8 ? (uint32_t)g : xv;
+        xh = o8 ? (uint32_t)(g >> 32) : xh;
       }
     }
-    isA = v == 0;
-    isB = v == 1;
-    valid = in_tab && start_ + o1 <= last;                        // snappy.c:143
-    vmask = ballot(valid);
-    p = valid ? start_ + o0 : 0;
-    if constexpr (IN::kWin) x.ensure(start_ + lane_val(o0, 63) + 16);  // lane 63: the last probe
-    xr = x.raw64(p);                                              // bytes p .. p+7
-  };
-  place(kv, start, false);
-  for (;;) {
-    uint64_t xw = xr.value();
-    if constexpr (IN::kWin) {
-      const bool op_ = valid & x.oow(p, 8);
-      if (ballot(op_)) xw = op_ ? x.g64(p) : xw;
-    }
-    const uint32_t xv = (uint32_t)xw;
-    const uint32_t hh = valid ? hash32(xv, shift) : kSink;
-    // snappy.c:146-148 (and :175, :179 for A and B) for all 64 probes at once.
-    uint32_t prev = tab_swap(tab, hh, p);
-    // The candidate's bytes are read before the order check, so the check
-    // runs under the read's latency (the rare path reads them again).
-    uint32_t yv = x.rd32(valid ? prev : 0);
-    if (ballot(valid & (prev > p))) {
+    h2 = (xv * kHashMul) >> hsh;                                  // snappy.c:44-47
+    ta = valid ? (h2 & ~3u) : kSinkOff;
+    sh = (h2 << 3) & 16u;
+    mask = 0xffffu << sh;
+    const uint32_t old = lds_mskor_rtn<TAB>(ta, mask, p << sh);   // snappy.c:146-148
+    prev = (old >> sh) & 0xffffu;
+    Raw32 yr = x.raw32(prev);                                     // the candidate's bytes
+    // (Checked under the read's latency; the rare path reads them again.)
+#ifdef LGS_PROBE_FORCE_REPLAY
+    // Probe build (tools/probe_ab.py): every batch takes the replay path, so
+    // the path that never runs on gfx950 is checked against the reference.
+    if (vmask) {
+#else
+    if (ballot(prev > p) & vmask) {
+#endif
       // Not in lane order (never seen on gfx950): put back each touched
       // slot's entry as the batch found it (the one lane per slot that
       // received a value from before the batch), then swap lane by lane.
-      const uint32_t p0 = lane_val(p, 0);
-      tab[(valid & (prev < p0)) ? hh : kSink] = (uint16_t)prev;
-      order();
+      const uint32_t p0 = lane_val(p, (uint32_t)__builtin_ctzll(vmask));
+      lds_mskor<TAB>(prev < p0 ? ta : kSinkOff, mask, prev << sh);
       for (uint64_t r = vmask; r; r &= r - 1) {
         const uint32_t l = (uint32_t)__builtin_ctzll(r);
-        const uint32_t got = tab_swap(tab, lane == l ? hh : kSink, p);
-        prev = lane == l ? got : prev;
+        const uint32_t got = lds_mskor_rtn<TAB>(lane == l ? ta : kSinkOff, mask, p << sh);
+        prev = lane == l ? (got >> sh) & 0xffffu : prev;
       }
-      yv = x.rd32(valid ? prev : 0);
+      yr = x.raw32(prev);
     }
+    uint32_t yv = yr.value();
     if constexpr (IN::kWin) {
-      const bool oc = valid & x.oow(prev, 4);
-      if (ballot(oc)) yv = oc ? x.g32(prev) : yv;
+      const bool o4 = valid & x.oow(prev, 4);
+      if (ballot(o4)) yv = o4 ? x.g32(prev) : yv;
     }
-    // snappy.c:152; A never matches; B is lcdb's 64-bit compare (snappy.c:182):
-    // bytes at..at+6 against a zero-extended 4-byte load.
-    const bool eq = xv == yv;
-    const bool hi0 = ((uint32_t)(xw >> 32) & 0xffffffu) == 0;
-    // (Bitwise, not ?: -- as a select chain on v the compiler lowers it
-    // to a divergent switch.)
-    const bool mt = eq & !isA & (!isB | hi0);
-    const uint64_t mm = ballot(mt) & vmask;
-
-    // The match path computes the copy's end; both paths then update the
-    // loop state with selects (one set of loop-carried values, no per-path
-    // copies of them at the latch).
-    uint32_t at_n = at;
-    bool done;
-    if (mm) {
+    // snappy.c:152; lane B: lcdb's 64-bit compare (snappy.c:182), bytes
+    // at..at+6 against a zero-extended 4-byte load; A never matches.
+    return ballot(((xv ^ yv) | (xh & pl.bm)) == 0) & vmask & ~1ull;
+  };
+  // A chunk's first batch: the post-copy layout from start = 1, A and B off.
+  bool evalid = (lane >= 2) & (pl.e1 <= last - 1);
+  p = evalid ? 1 + pl.e0 : 0;
+  if constexpr (IN::kWin) x.ensure(1 + kPostLast + 16);
+  xr = x.raw64(p);
+  for (;;) {
+    const uint32_t at_in = at;
+    // Rotated: the batch is the loop's last step, so its match test is the
+    // loop's only exit (a test in the middle became a selector variable).
+    for (uint64_t mm = batch(evalid); mm;
+         mm = batch((int32_t)(last - start) >= (int32_t)pl.e1)) {
+      // ---- the copy (snappy.c:156-169)
       const uint32_t m = (uint32_t)__builtin_ctzll(mm);           // the matching probe
       const uint32_t base = lane_val(p, m);
       const uint32_t ref = lane_val(prev, m);
       // The probes after it did not happen: in each slot they touched, the
-      // first of them puts back what it received.
-      tab[(valid & (lane > m) & (prev <= base)) ? hh : kSink] = (uint16_t)prev;
-      order();
-      // ---- the copy (snappy.c:158-169)
-      uint32_t r = ref + 4;
-      at_n = base + 4;
+      // first of them puts back what it received.  A plain u16 store: the
+      // lanes with nothing to put back all aim at the sink, and same-address
+      // LDS atomics serialise where same-address stores do not (as an
+      // ds_mskor this store took bank conflicts per launch from 1.0e8 to
+      // 2.5e8, profiles/r4b_pmc_mskor_restore.txt).
+      // (Lanes that are no probe have ta at the sink: their received value
+      // is the sink's and must not reach a real entry.)
+      *reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(tab) +
+                                   (((lane > m) & (prev <= base)) ? (ta | (h2 & 2u)) : kSinkOff)) =
+          (uint16_t)prev;
+      const uint32_t dist = base - ref;
+      uint32_t at_n = base + 4;
 #pragma clang loop unroll(disable)
       for (;;) {                                                  // snappy.c:163-164
         const uint32_t q = at_n + lane;
         if constexpr (IN::kWin) x.ensure(at_n + kWave);
         // Unconditional reads, unclamped: lanes at q >= n read at most 63
         // bytes past the chunk (the LDS image has that slack; the window
-        // ring masks its index) and their bytes are discarded by `same`.
-        // (r + lane < q: the source starts before the copy.)
-        const uint32_t qa = q, ra = r + lane;
-        uint32_t br = x.byte(ra), bq = x.byte(qa);
+        // ring masks its index), and count as a mismatch.
+        uint32_t bq = x.byte(q), br = x.byte(q - dist);
         if constexpr (IN::kWin) {
-          const bool orq = (q < n) & (x.oow(ra, 1) || x.oow(qa, 1));
+          const bool orq = x.oow(q - dist, 1) || x.oow(q, 1);
           if (ballot(orq)) {
-            br = orq ? x.gbyte(ra) : br;
-            bq = orq ? x.gbyte(qa) : bq;
+            br = orq ? x.gbyte(q - dist) : br;
+            bq = orq ? x.gbyte(q) : bq;
           }
         }
-        const bool same = (q < n) & (br == bq);
-        const uint64_t diff = ballot(!same);
+        const uint64_t diff = ballot(br != bq) | ballot(q >= n);
         if (diff) {
           at_n += (uint32_t)__builtin_ctzll(diff);
           break;
         }
         at_n += kWave;
-        r += kWave;
       }
-      // Match: the search restarts after the copy (snappy.c:169, 184-185).
-      done = at_n >= last;
-      place(0u, at_n + 1, false);       // (also when done: harmless, and no copies at the latch)
-
+      // The batch after the copy (snappy.c:172-186 + the next search): its
+      // read goes out now, under the op's bookkeeping.  Past the limit
+      // (snappy.c:169) no lane of it is on, so it finds no match and ends the
+      // chunk.
+      start = at_n + 1;
+      p = start + pl.e0;
+      if constexpr (IN::kWin) x.ensure(start + kPostLast + 16);
+      xr = x.raw64(p);
       // snappy.c:156 + 166: the literal before the copy (empty after a
       // re-match), then the copy -- recorded, emitted by flush_ops.
-      const uint32_t clen = at_n - base, dist = base - ref;
-      write_lane2(recA, (base << 16) | clen, recB, dist, nops);
-      if (++nops == kWave) {                                      // every 64 ops
+      at = at_n;
+      rec_lane(recA, base | (at_n << 16), sel);
+      rec_lane(recB, ref, sel);
+      sel <<= 1;
+      if (!sel) {                                                 // every 64 ops
         op = flush_ops(o, op, x, recA, recB, kWave, lit0);
-        nops = 0;
+        sel = 1;
         lit0 = at_n;
       }
-    } else {
-      // No match: the search ends if a probe of the batch was past the limit
-      // (snappy.c:143), else continues with the next 64 probes.
-      done = vmask != ~0ull;
-      place(kv + kWave, start, done);
     }
-    lit = mm ? at_n : lit;
-    start = mm ? at_n + 1 : start;
-    kv = mm ? 0u : kv + kWave;
-    at = at_n;
-    if (done) break;
+    if (at >= last) break;
+    // No match in the batch: the search ends if a probe of the batch was
+    // past the limit (snappy.c:143), else continues with its next 62 probes,
+    // from the probe table.
+    if ((vmask | 3ull) != ~0ull) break;
+    kb = (at != at_in ? 0u : kb) + kProbesPerBatch;
+    const uint32_t kk = kb + lane - 2;
+    const bool in_tab = (lane >= 2) & (kk < kProbeTab);
+    const uint32_t kc = in_tab ? kk : 0u;
+    const uint32_t o0 = kProbe.off[kc], o1 = kProbe.off[kc + 1];
+    // Wait for these two loads here, on the rare path.  Left to the
+    // compiler, the wait lands where the paths merge as vmcnt(0) -- and
+    // vmcnt also counts the output stores, so every batch would stall
+    // until the previous copy's bytes had reached memory.
+    __builtin_amdgcn_s_waitcnt(0x0f70);                           // vmcnt(0)
+    evalid = in_tab & (o1 <= last - start);                       // snappy.c:143
+    p = evalid ? start + o0 : 0;
+    if constexpr (IN::kWin) x.ensure(start + lane_val(o0, kWave - 1) + 16);
+    xr = x.raw64(p);
   }
+  const uint32_t nops = (uint32_t)__builtin_ctzll(sel);
   if (nops) op = flush_ops(o, op, x, recA, recB, nops, lit0);
 
-  if (lit < n) op += emit_literal(o, op, x, lit, n - lit);         // snappy.c:190-192
+  if (at < n) op += emit_literal(o, op, x, at, n - at);           // snappy.c:190-192
   return op;
-}
-
-// Offsets, relative to the batch's start = at + 1, of each lane's probe in
-// the batch right after a copy: lane 0 is the re-probe's A (at - 1), lane 1
-// its B (at), lane l >= 2 search probe l - 2; e1 is the offset of the probe
-// after it (the bound check of snappy.c:143; A and B always pass it, the
-// batch runs only while at < last).
-__device__ __forceinline__ void post_copy_offsets(uint32_t lane, uint32_t* e0, uint32_t* e1) {
-  const uint32_t pk = lane >= 2 ? lane - 2 : 0;
-  *e0 = lane == 0 ? 0xfffffffeu : (lane == 1 ? 0xffffffffu : probe_off(pk));
-  *e1 = lane < 2 ? 0u : probe_off(pk + 1);
 }
 
 // varint32 header hv (coding.h:140-167) at the slot's start, unless hv is
@@ -681,36 +704,43 @@ __device__ __forceinline__ OutSlot out_slot(uint8_t* out, uint64_t off, uint32_t
                                                    0x00020000)};
 }
 
-// Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].  hdr == nullptr: item is a whole block, prefixed with
-// its varint32 length (snappy.c:368).  Otherwise hdr[i] is the varint value
-// to prefix, or 0xffffffff for none (a later chunk of a > 64 KiB block).
-template <uint32_t IN_CAP, uint32_t WAVES>
-__global__ __launch_bounds__(64 * WAVES) void encode_kernel(
+// One wave's LDS: the chunk image at LDS 0 (its reads need no base: a
+// ds_read2_b32 offset reaches only 1 KiB), then the hash table and its sink
+// at the constant offset IMG, which the table's LDS atomics carry in their
+// 16-bit offset field.  Each kernel declares this as its only __shared__
+// object, so it is placed at LDS 0 (checked at the kernel's start).
+template <uint32_t IMG>
+struct EncLds {
+  static_assert(IMG % 16 == 0 && IMG <= 65535 - 2 * kSink - 16, "table offset");
+  uint8_t img[IMG];
+  uint16_t tab[kTableCap + 8];                        // + the sink
+};
+
+// Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].
+// hdr == nullptr: item is a whole block, prefixed with its varint32 length
+// (snappy.c:368).  Otherwise hdr[i] is the varint value to prefix, or
+// 0xffffffff for none (a later chunk of a > 64 KiB block).  One wave per
+// work item, one-wave workgroups (a static partition over persistent waves
+// balances worse).
+template <uint32_t IN_CAP>
+__global__ __launch_bounds__(64) void encode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
     const uint32_t* __restrict__ count) {
-  // + 48: the zero granule past the image (and spare); + 64: the match extension's reads
-  // past the chunk (encode_chunk).  8 832 B with the table: still 18 waves
-  // per CU (the 1 280-byte LDS granule).
-  __shared__ __attribute__((aligned(16))) uint8_t s_in[WAVES][IN_CAP + 112];
-  __shared__ __attribute__((aligned(16))) uint16_t s_tab[WAVES][kTableCap + 8];   // + sink
+  // Image: + 48 the zero granule past it (and spare), + 64 the match
+  // extension's reads past the chunk (encode_chunk).  8 832 B with the
+  // table: 18 waves per CU (the 1 280-byte LDS granule).
+  constexpr uint32_t kImg = IN_CAP + 112;
+  __shared__ __attribute__((aligned(16))) EncLds<kImg> s;
+  if (lds_addr(&s) != 0) __builtin_trap();            // encode_chunk<kImg> assumes it
 
-  // Per-wave scalars go through v_readfirstlane so hipcc keeps the control
-  // flow on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
-  const uint32_t wv = uni(threadIdx.x >> 6);
-  const uint32_t slot = blockIdx.x * WAVES + wv;
+  const uint32_t slot = blockIdx.x;
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
-  // Probe offsets of search probes lane - 2 (the batch right after a copy,
-  // whose lanes 0 and 1 are the re-probe), kept in registers.  Relative
-  // to that batch's start = at + 1 the re-probe's positions are A = at - 1
-  // (offset -2) and B = at (-1), and both are always in bounds (the batch
-  // runs only while at < last): offset 0 for their bound check.
-  uint32_t e0, e1;
-  post_copy_offsets(lane, &e0, &e1);
+  const PostLanes pl = post_lanes(lane);
 
   const uint32_t len = uni(in_len[i]);
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
@@ -722,15 +752,15 @@ __global__ __launch_bounds__(64 * WAVES) void encode_kernel(
   // (IN_CAP >= min(len, 65536) is guaranteed by the launcher.)
   for (uint32_t c0 = 0; c0 < len; c0 += kChunk) {
     const uint32_t clen = len - c0 < kChunk ? len - c0 : kChunk;
-    // Byte k of the chunk at s_in[k]: the image's dword reads are aligned
+    // Byte k of the chunk at img[k]: the image's dword reads are aligned
     // for any input alignment (unaligned LDS dword reads took C2 encode from
     // 0.78 to 1.5 ms, see LdsIn).
     constexpr uint32_t kR = (IN_CAP + 16 + 1023) / 1024 < 8 ? (IN_CAP + 16 + 1023) / 1024 : 8;
-    stage_in_linear<kR>(&s_in[wv][0], src + c0, clen);
-    LdsIn x{&s_in[wv][0]};
+    stage_in_linear<kR>(s.img, src + c0, clen);
+    LdsIn x{s.img};
     order();
     if (clen >= kMinBlock) {
-      op = encode_chunk(x, clen, &s_tab[wv][0], o, op, e0, e1);
+      op = encode_chunk<kImg>(x, clen, s.tab, o, op, pl);
     } else {
       op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
@@ -749,15 +779,14 @@ __global__ __launch_bounds__(64) void encode_win_kernel(
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
     const uint32_t* __restrict__ count) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[W + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t s_tab[kTableCap + 8];   // + sink
+  __shared__ __attribute__((aligned(16))) EncLds<W + 16> s;    // ring + its 16-byte mirror
+  if (lds_addr(&s) != 0) __builtin_trap();            // encode_chunk<W + 16> assumes it
 
   const uint32_t slot = blockIdx.x;
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
   const uint32_t lane = lane_id();
-  uint32_t e0, e1;
-  post_copy_offsets(lane, &e0, &e1);
+  const PostLanes pl = post_lanes(lane);
   const uint32_t len = uni(in_len[i]);
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
   const OutSlot o = out_slot(out, uni64(out_off[i]), len);
@@ -766,10 +795,10 @@ __global__ __launch_bounds__(64) void encode_win_kernel(
     const uint32_t clen = len - c0 < kChunk ? len - c0 : kChunk;
     const gptr<const uint8_t> g = src + c0;
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
-    WinIn<W> x{s_ring, g - sh, sh, clen, 0};
+    WinIn<W> x{s.img, g - sh, sh, clen, 0};
     if (clen >= kMinBlock) {
       x.ensure(W / 4);
-      op = encode_chunk(x, clen, s_tab, o, op, e0, e1);
+      op = encode_chunk<W + 16>(x, clen, s.tab, o, op, pl);
     } else {
       op += emit_literal(o, op, x, 0, clen);                    // snappy.c:379-380
     }
@@ -779,16 +808,12 @@ __global__ __launch_bounds__(64) void encode_win_kernel(
   if (lane == 0) out_len[i] = op;
 }
 
-#ifndef LGS_ENC_WIN
-#define LGS_ENC_WIN 1
-#endif
 // The 64 KiB class (and longer blocks, chunk by chunk).
 static hipError_t launch_encode_big(const EncodeArgs& a, hipStream_t s);
 
-template <uint32_t IN_CAP, uint32_t WAVES>
+template <uint32_t IN_CAP>
 static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
-  const uint32_t grid = (a.n + WAVES - 1) / WAVES;
-  hipLaunchKernelGGL((encode_kernel<IN_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s, a.in,
+  hipLaunchKernelGGL((encode_kernel<IN_CAP>), dim3(a.n), dim3(64), 0, s, a.in,
                      a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
                      a.count);
   return hipGetLastError();
@@ -805,13 +830,11 @@ static hipError_t launch_encode_small(const EncodeArgs& a, hipStream_t s) {
   // C2: a wave's wait for its next block also drains its previous block's
   // output stores (vmcnt counts both), and a static partition of blocks over
   // waves balances worse than dispatching one-wave workgroups.)
-  return launch_encode_cls<kEncCap0, 1>(a, s);
+  return launch_encode_cls<kEncCap0>(a, s);
 }
 constexpr uint32_t kEncCap1 = 16896;
-constexpr uint32_t kEncCap2 = 65536;
 
 static hipError_t launch_encode_big(const EncodeArgs& a, hipStream_t s) {
-  if (!LGS_ENC_WIN) return launch_encode_cls<kEncCap2, 1>(a, s);
   hipLaunchKernelGGL((encode_win_kernel<32768>), dim3(a.n), dim3(64), 0, s, a.in, a.in_off,
                      a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n, a.count);
   return hipGetLastError();
@@ -823,7 +846,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
   if (max_in <= kEncCap0) return launch_encode_small(a, s);
   if (a.index || a.n < kSplitMinBlocks || !options().split) {
-    if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1, 1>(a, s);
+    if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1>(a, s);
     return launch_encode_big(a, s);
   }
   // A mixed-size batch: each size class in its own kernel (see
@@ -842,7 +865,7 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   c.index = list; c.count = cnt;
   if ((e = launch_encode_small(c, s)) != hipSuccess) return e;
   c.index = list + a.n; c.count = cnt + 1;
-  if ((e = launch_encode_cls<kEncCap1, 1>(c, s)) != hipSuccess) return e;
+  if ((e = launch_encode_cls<kEncCap1>(c, s)) != hipSuccess) return e;
   c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
   if (max_in > kEncCap1 && (e = launch_encode_big(c, s)) != hipSuccess) return e;
   return scratch.release();

@@ -288,6 +288,50 @@ def test_misaligned_blocks_c1_round_trip(gpu, digests, force, shift):
         assert corpus.digest_of_digests(corpus.block_digests(ho.buf, ho.off, ho.len)) == d["raw_dd"]
 
 
+def test_encode_block_flush_with_allocation_end(gpu):
+    # lgs_encode_batch_dev promises no read slack, so a block whose
+    # last byte is the last byte of its device allocation must be encoded
+    # from inside it (the staging reads a ragged last granule as the 16 bytes
+    # ending at the block's end, and a block under 16 bytes a byte per lane).
+    # Every length residue mod 16, each block alone at the end of its own
+    # page-multiple hipMalloc, against the reference encoder.
+    import ctypes as C
+    import torch
+    from lcdb_amd import _native
+    hip = C.CDLL("libamdhip64.so")
+    ref = oracle.best()
+    lib = _native.lib()
+    rng = np.random.default_rng(0xF1)
+    fill = corpus.fillseq(20)
+    lengths = list(range(1, 49)) + [4096 + k for k in range(-16, 17)] + \
+        [16384 + 9, 65536 - 5, 65536, 65536 + 7, 70001]
+    for L in lengths:
+        raw = bytes(fill.buf[:L]) if L <= len(fill.buf) else bytes(rng.integers(0, 4, L, dtype=np.uint8))
+        size = (L + 4095) // 4096 * 4096
+        p = C.c_void_p()
+        assert hip.hipMalloc(C.byref(p), C.c_size_t(size)) == 0
+        try:
+            src = np.frombuffer(raw, dtype=np.uint8)
+            assert hip.hipMemcpy(C.c_void_p(p.value + size - L), C.c_void_p(src.ctypes.data),
+                                 C.c_size_t(L), 1) == 0
+            off = torch.tensor([size - L], dtype=torch.int64, device="cuda")
+            ln = torch.tensor([L], dtype=torch.int32, device="cuda")
+            out = torch.zeros(gpu.encode_bound(L) + 16, dtype=torch.uint8, device="cuda")
+            ooff = torch.zeros(1, dtype=torch.int64, device="cuda")
+            olen = torch.zeros(1, dtype=torch.int32, device="cuda")
+            s = torch.cuda.current_stream()
+            _native.check(lib.lgs_encode_batch_dev(p.value, off.data_ptr(), ln.data_ptr(),
+                                                   out.data_ptr(), ooff.data_ptr(),
+                                                   olen.data_ptr(), 1, L, s.cuda_stream),
+                          "lgs_encode_batch_dev")
+            s.synchronize()
+            got = out[:int(olen.item())].cpu().numpy().tobytes()
+            assert got == ref.encode(raw), L
+        finally:
+            torch.cuda.synchronize()
+            hip.hipFree(p)
+
+
 def test_encode_c2_and_random(gpu, digests):
     # The encoder on the full C2 corpus, then on random, zero, periodic and
     # short inputs of every length class in one batch.

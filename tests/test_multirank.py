@@ -168,11 +168,15 @@ def test_cpu_baseline_fields_on_cpu():
         buf, off, len = out, ooff, olen
     cb = bench.cpu_baseline(c, a, H, 1)
     nproc = len(os.sched_getaffinity(0))
-    assert cb["threads"] == nproc and cb["nproc"]["threads"] == nproc
+    assert cb["nproc"]["threads"] == nproc
     assert cb["single_thread"]["threads"] == 1 and cb["per_gpu_share"]["threads"] == 2
     assert 1 <= cb["cores"] <= nproc
     assert cb["same_bytes_as_gpu"] is True
-    assert cb["value"] == cb["nproc"]["roundtrip_GiBps"] > 0
+    # the headline is the fastest of the three points (on a small sample or
+    # under a CPU quota fewer threads can win), and says which one it is
+    pts = [cb["single_thread"], cb["per_gpu_share"], cb["nproc"]]
+    assert cb["value"] == max(x["roundtrip_GiBps"] for x in pts) > 0
+    assert cb["threads"] in {x["threads"] for x in pts}
     if nproc > 1:
         assert set(cb["nproc"]["by_partition"]) == {"round-robin", "contiguous"}
 
