@@ -306,17 +306,13 @@ int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
                          size_t *slot_bytes);
 
 /* Process-wide kernel choices (A/B and tests; the defaults pick by batch):
-     "decoder": "auto" | "ops" (two passes: a lane per block walks the tags
-                into op lists, a wave per block executes them; outputs of
-                the 4 608-byte class, larger ones go to the defaults)
-                | "ring" (lane-per-block) | "wave" (wave-per-block)
-                | "quad" (four lanes per block; A/B only)
-     "wide":    "walk" (default) | "trips"  (decoder of outputs over 16 KiB:
-                the one-tag walk, or up to 8 tags per step; A/B only)
+     "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
+     "wide":    "walk"  (decoder of outputs over 16 KiB: the one-tag walk)
      "split":   "1" | "0"  (size-class split of mixed batches, see above)
-   Initial values: LGS_DECODE_KERNEL, LGS_WIDE_DECODER, LGS_NO_SPLIT=1, read
-   once at load.
-   LGS_EINVAL for an unknown name or value. */
+   Initial values: LGS_DECODE_KERNEL, LGS_NO_SPLIT=1, read once at load.
+   LGS_EINVAL for an unknown name or value.  (The decoders that lost their
+   A/B -- "decoder" "quad" and "ops", "wide" "trips" -- exist only in the
+   test-only probe library; this library rejects them.) */
 int lgs_set_option(const char *name, const char *value);
 
 /* HBM yardstick, not part of the codec: copies `bytes` (a multiple of 16)

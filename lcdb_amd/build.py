@@ -21,16 +21,22 @@ PKG = os.path.join(ROOT, "lcdb_amd")
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "liblcdb_gpu_snappy.so")
 CORPUS_LIB = os.path.join(PKG, "libcorpus.so")
+# Test-only: the product sources plus the decoders that lost their A/B
+# (lgs_decode_probe.hip, -DLGS_PROBE_DECODERS).  Never loaded by lcdb or the
+# product path; tests/test_gpu_probe_decoders.py runs it in a subprocess.
+PROBE_LIB = os.path.join(PKG, "liblcdb_gpu_snappy_probe.so")
+PROBE_SOURCES = ["lgs_decode_probe.hip"]
 
 HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip",
                "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp", "lgs_probe.hip"]
-HIP_HEADERS = ["lgs_device.h", "lgs_launch.h"]
+HIP_HEADERS = ["lgs_device.h", "lgs_launch.h", "lgs_decode_common.h"]
 # Only ldb_snappy_* and lgs_* are exported (the library is loaded into lcdb).
 EXPORTS_MAP = os.path.join(CSRC, "exports.map")
 # The files that define the two profiled codec kernels and how they are
 # launched (grid, LDS class, split); the host runtime, table and bloom
 # sources do not change what encode_kernel / decode_ring_kernel execute.
-CODEC_KERNEL_FILES = ["lgs_encode.hip", "lgs_decode.hip", "lgs_device.h", "lgs_launch.h"]
+CODEC_KERNEL_FILES = ["lgs_encode.hip", "lgs_decode.hip", "lgs_device.h", "lgs_launch.h",
+                      "lgs_decode_common.h"]
 ARCH = "gfx950"
 
 
@@ -79,6 +85,15 @@ def build_hip(force: bool = False, extra: list[str] | None = None, out: str = LI
     return out
 
 
+def build_probe(force: bool = False) -> str:
+    """The probe library (tests only): product sources + lgs_decode_probe.hip."""
+    deps = [os.path.join(CSRC, s) for s in PROBE_SOURCES]
+    if force or _stale(PROBE_LIB, deps + [LIB]):
+        build_hip(force=True, out=PROBE_LIB,
+                  extra=["-DLGS_PROBE_DECODERS"] + deps)
+    return PROBE_LIB
+
+
 def build_corpus(force: bool = False) -> str:
     src = os.path.join(CSRC, "corpus.c")
     if force or _stale(CORPUS_LIB, [src]):
@@ -103,6 +118,7 @@ def build_all(force: bool = False) -> None:
     build_corpus(force)
     build_oracle()
     build_hip(force)
+    build_probe(force)
     build_lcdb_harness()
 
 

@@ -727,12 +727,14 @@ Options& options_init() {
     const char* dk = getenv("LGS_DECODE_KERNEL");
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
+#ifdef LGS_PROBE_DECODERS
     if (dk && !strcmp(dk, "quad")) v->decoder = kDecQuad;
     if (dk && !strcmp(dk, "ops")) v->decoder = kDecOps;
-    const char* ns = getenv("LGS_NO_SPLIT");
-    if (ns && *ns && strcmp(ns, "0")) v->split = 0;
     const char* wd = getenv("LGS_WIDE_DECODER");
     if (wd && !strcmp(wd, "trips")) v->wide = kWideTrips;
+#endif
+    const char* ns = getenv("LGS_NO_SPLIT");
+    if (ns && *ns && strcmp(ns, "0")) v->split = 0;
     return v;
   }();
   return *o;
@@ -804,9 +806,13 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
+#ifdef LGS_PROBE_DECODERS
+    // The decoders that lost their A/B exist in the probe library only
+    // (lgs_decode_probe.hip); the product rejects them.
     else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
     else if (!strcmp(value, "ops")) o.decoder = kDecOps;
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, ops, ring, quad or wave)", value);
+#endif
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)
@@ -819,8 +825,10 @@ int lgs_set_option(const char* name, const char* value) {
   }
   if (!strcmp(name, "wide")) {
     if (!strcmp(value, "walk") || !*value) o.wide = kWideWalk;
+#ifdef LGS_PROBE_DECODERS
     else if (!strcmp(value, "trips")) o.wide = kWideTrips;
-    else return fail(LGS_EINVAL, "wide '%s' (walk or trips)", value);
+#endif
+    else return fail(LGS_EINVAL, "wide '%s' (walk)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "split")) {

@@ -534,8 +534,9 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   uint32_t p;
   uint64_t vmask = 0;
   Raw64 xr;
-  // The batch's table state, kept for the copy that follows a match.
-  uint32_t prev = 0, h2 = 0, ta = 0, sh = 0, mask = 0;
+  // The batch's table state, kept for the copy that follows a match, and
+  // each lane's bytes 4..7 of probe against candidate (0: they match).
+  uint32_t prev = 0, h2 = 0, ta = 0, sh = 0, mask = 0, d47 = 0;
   // ---- one batch: snappy.c:146-152 for its 64 probes, `valid` the lanes
   // that are probes.  Returns the lanes that match.  (Validity is passed in,
   // not kept: a bool carried around the loop becomes a lane-mask phi merged
@@ -557,7 +558,7 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     mask = 0xffffu << sh;
     const uint32_t old = lds_mskor_rtn<TAB>(ta, mask, p << sh);   // snappy.c:146-148
     prev = (old >> sh) & 0xffffu;
-    Raw32 yr = x.raw32(prev);                                     // the candidate's bytes
+    Raw64 yr = x.raw64(prev);                                     // the candidate's bytes
     // (Checked under the read's latency; the rare path reads them again.)
 #ifdef LGS_PROBE_FORCE_REPLAY
     // Probe build (tools/probe_ab.py): every batch takes the replay path, so
@@ -576,13 +577,18 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
         const uint32_t got = lds_mskor_rtn<TAB>(lane == l ? ta : kSinkOff, mask, p << sh);
         prev = lane == l ? (got >> sh) & 0xffffu : prev;
       }
-      yr = x.raw32(prev);
+      yr = x.raw64(prev);
     }
-    uint32_t yv = yr.value();
+    uint32_t yv = yr.lo(), yh = yr.hi();
     if constexpr (IN::kWin) {
-      const bool o4 = valid & x.oow(prev, 4);
-      if (ballot(o4)) yv = o4 ? x.g32(prev) : yv;
+      const bool o8 = valid & x.oow(prev, 8);
+      if (ballot(o8)) {
+        const uint64_t g = x.g64(prev);
+        yv = o8 ? (uint32_t)g : yv;
+        yh = o8 ? (uint32_t)(g >> 32) : yh;
+      }
     }
+    d47 = xh ^ yh;
     // snappy.c:152; lane B: lcdb's 64-bit compare (snappy.c:182), bytes
     // at..at+6 against a zero-extended 4-byte load; A never matches.
     return ballot(((xv ^ yv) | (xh & pl.bm)) == 0) & vmask & ~1ull;
@@ -614,9 +620,14 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
                                    (((lane > m) & (prev <= base)) ? (ta | (h2 & 2u)) : kSinkOff)) =
           (uint16_t)prev;
       const uint32_t dist = base - ref;
-      uint32_t at_n = base + 4;
+      // Bytes 4..7 were compared in the batch (the candidate's read took
+      // its third dword): a copy shorter than 8 bytes ends there, with no
+      // extension round trip.  (Probe and candidate both lie at least 15
+      // bytes before the chunk's end, snappy.c:106, so all 8 are inside.)
+      const uint32_t e47 = lane_val(d47, m);
+      uint32_t at_n = base + 4 + (e47 ? (uint32_t)__builtin_ctz(e47) >> 3 : 4u);
 #pragma clang loop unroll(disable)
-      for (;;) {                                                  // snappy.c:163-164
+      for (; !e47;) {                                             // snappy.c:163-164
         const uint32_t q = at_n + lane;
         if constexpr (IN::kWin) x.ensure(at_n + kWave);
         // Unconditional reads, unclamped: lanes at q >= n read at most 63

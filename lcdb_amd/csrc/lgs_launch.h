@@ -41,6 +41,15 @@ struct EncodeArgs {
 
 // max_out: largest out_cap in the launch (selects the LDS class).
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
+#ifdef LGS_PROBE_DECODERS
+// Probe library only (lgs_decode_probe.hip): the decoders that lost their
+// A/B, selectable through lgs_set_option for tests and measurements.
+hipError_t launch_decode_quad(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_decode_ops(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s);
+#endif
+// The ring decoder (lane per block, large batches), for the split launch.
+hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
 // max_in: largest item length in the launch (<= 65536).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s);
 // Sort a mixed-size batch into size classes on the device: class c holds

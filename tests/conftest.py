@@ -24,16 +24,24 @@ import golden_io  # noqa: E402
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X GPU (run with -m gpu)")
     config.addinivalue_line("markers", "slow: multi-second CPU test")
+    config.addinivalue_line("markers", "probe: covers a probe-library decoder (LGS_TEST_PROBE=1)")
 
 
 def _ensure_built():
     from lcdb_amd import build
-    need = [build.LIB, build.CORPUS_LIB, os.path.join(ROOT, "oracle", "liboracle.so")]
+    need = [build.LIB, build.PROBE_LIB, build.CORPUS_LIB,
+            os.path.join(ROOT, "oracle", "liboracle.so")]
     if not all(os.path.exists(p) for p in need):
         build.build_all()
 
 
 _ensure_built()
+
+if os.environ.get("LGS_TEST_PROBE") == "1":
+    # tests/test_gpu_probe_decoders.py: this process tests the probe library
+    # (product sources + the decoders that lost their A/B).
+    from lcdb_amd import build as _build
+    _build.LIB = _build.PROBE_LIB
 
 
 @pytest.fixture(scope="session")

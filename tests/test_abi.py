@@ -116,3 +116,23 @@ def test_integration_recipe_names_the_built_sources():
     assert "--version-script=lcdb_amd/csrc/exports.map" in block
     for s in named:
         assert os.path.exists(os.path.join(ROOT, "lcdb_amd", "csrc", s))
+
+
+def test_product_has_only_the_kept_decoders():
+    """the decoders that lost their A/B (quad, two-pass, trips)
+    live in the probe library only.  The product library neither contains
+    their kernels nor accepts their options (lgs_set_option needs no GPU)."""
+    blob = open(build.LIB, "rb").read()
+    for k in (b"decode_quad_kernel", b"tag_scan_kernel", b"op_exec_kernel",
+              b"decode_trips_kernel"):
+        assert k not in blob, k
+    for k in (b"decode_ring_kernel", b"decode_wide_kernel", b"decode_kernel"):
+        assert k in blob, k
+    lib = _native.lib()
+    for name, value in (("decoder", "quad"), ("decoder", "ops"), ("wide", "trips")):
+        assert lib.lgs_set_option(name.encode(), value.encode()) == _native.LGS_EINVAL, value
+    for name, value in (("decoder", "ring"), ("decoder", "wave"), ("decoder", "auto"),
+                        ("wide", "walk")):
+        assert lib.lgs_set_option(name.encode(), value.encode()) == _native.LGS_OK, value
+    probe = open(build.PROBE_LIB, "rb").read()
+    assert b"decode_quad_kernel" in probe and b"op_exec_kernel" in probe

@@ -4,6 +4,7 @@ reference encoder, decoded bytes identical, accept/reject identical."""
 from __future__ import annotations
 
 import hashlib
+import os
 import threading
 
 import numpy as np
@@ -13,6 +14,16 @@ import oracle
 from lcdb_amd import corpus
 
 pytestmark = pytest.mark.gpu
+
+# LGS_TEST_PROBE=1 (tests/test_gpu_probe_decoders.py runs this file so in a
+# subprocess): the library is the probe build (conftest.py), and the tests
+# below also cover the decoders that lost their A/B and exist only there.
+PROBE = os.environ.get("LGS_TEST_PROBE") == "1"
+
+
+def _with_probe(kernels, probe_kernels):
+    return list(kernels) + [pytest.param(k, marks=pytest.mark.probe) for k in probe_kernels
+                            if PROBE]
 
 
 def test_dropin_encode_golden(gpu, vectors):
@@ -197,7 +208,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "ring", "quad", "ops"])
+@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops"]))
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -216,7 +227,8 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-def test_decode_kernels_c2_full_size(gpu, digests, force):
+@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops")]))
+def test_decode_kernels_c2_full_size(gpu, digests, force, kernels):
     import torch
     from lcdb_amd import batch
     d = digests["C2_fillseq_65536x4KiB"]
@@ -224,7 +236,7 @@ def test_decode_kernels_c2_full_size(gpu, digests, force):
     raw = batch.upload(c)
     comp = batch.encode_slots(raw)
     batch.encode(raw, comp)
-    for kernel in ("ring", "wave", "quad", "ops"):
+    for kernel in kernels:
         force("decoder", kernel)
         out = batch.decode_slots(c.len)
         st = torch.zeros(c.n, dtype=torch.uint8, device="cuda")
@@ -367,7 +379,7 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", ["ring", "quad", "ops"])
+@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops"]))
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
@@ -439,7 +451,7 @@ def _header(s: bytes):
     return None
 
 
-def test_decode_ops_rejects_overflow_and_jumps(gpu, vectors, force):
+def _decode_ops_rejects_overflow_and_jumps(gpu, vectors, force):
     # The two-pass decoder (ops) on its own class, every outcome against the
     # reference: the golden compressed streams (corrupt ones included) at a
     # 4 608-byte capacity; 3 000 corruptions of fillseq blocks (byte flips,
@@ -494,7 +506,13 @@ def test_decode_ops_rejects_overflow_and_jumps(gpu, vectors, force):
             assert code == gpu.LGS_ST_CORRUPT, k
 
 
-@pytest.mark.parametrize("kernel", [None, "ring", "quad", "ops"])
+if PROBE:   # the two-pass decoder exists in the probe library only
+    test_decode_ops_rejects_overflow_and_jumps = pytest.mark.probe(
+        _decode_ops_rejects_overflow_and_jumps)
+
+
+
+@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops"]))
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
@@ -580,7 +598,7 @@ def _copy2(length: int, dist: int) -> bytes:
     return bytes([((length - 1) << 2) | 2, dist & 255, dist >> 8])
 
 
-@pytest.mark.parametrize("wide", ["trips", "walk"])
+@pytest.mark.parametrize("wide", _with_probe(["walk"], ["trips"]))
 def test_decode_wide_far_copies_long_literals_and_rejects(gpu, force, wide):
     # Outputs over the 16 KiB class go to the wide decoders (a 32 KiB output
     # ring flushed to HBM, a 4 KiB stream ring refilled 2 KiB at a time; the
@@ -693,7 +711,7 @@ def _trip_stress_stream(rng, want: int) -> bytes:
     return _varint(len(out)) + bytes(s), bytes(out)
 
 
-@pytest.mark.parametrize("wide", ["trips", "walk"])
+@pytest.mark.parametrize("wide", _with_probe(["walk"], ["trips"]))
 def test_decode_wide_dependent_copies_and_c3(gpu, digests, force, wide):
     # The wide class (outputs over 16 KiB) on C3 (its 64 KiB fillseq and
     # random classes among the others) and on hand-made streams dense in
