@@ -38,6 +38,12 @@ EXPORTS_MAP = os.path.join(CSRC, "exports.map")
 CODEC_KERNEL_FILES = ["lgs_encode.hip", "lgs_decode.hip", "lgs_device.h", "lgs_launch.h",
                       "lgs_decode_common.h"]
 ARCH = "gfx950"
+# If-conversion thresholds: hipcc's defaults leave small two-way branches as
+# exec-mask regions; these fold them into selects (the ring decoder's trip:
+# 84 -> 70 s_and_saveexec regions; C2 decode 280 -> 274 us, encode unchanged,
+# profiles/r4f_session.txt).
+FOLD_FLAGS = ["-mllvm", "-phi-node-folding-threshold=8",
+              "-mllvm", "-two-entry-phi-node-folding-threshold=16"]
 
 
 def kernel_sources_sha() -> str:
@@ -49,6 +55,7 @@ def kernel_sources_sha() -> str:
     for name in sorted(CODEC_KERNEL_FILES):
         with open(os.path.join(CSRC, name), "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
+    h.update(" ".join(FOLD_FLAGS).encode())
     return h.hexdigest()[:16]
 
 
@@ -79,7 +86,7 @@ def build_hip(force: bool = False, extra: list[str] | None = None, out: str = LI
     if force or _stale(out, deps):
         tmp = out + ".tmp"
         _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wextra", "-pthread", f"-Wl,--version-script={EXPORTS_MAP}", *srcs,
+              "-Wall", "-Wextra", "-pthread", *FOLD_FLAGS, f"-Wl,--version-script={EXPORTS_MAP}", *srcs,
               "-o", tmp, *(extra or [])])
         os.replace(tmp, out)
     return out

@@ -3,26 +3,34 @@
 // snappy.c:364-384 (snappy_encode).
 //
 // One wave owns one work item (a whole block <= 64 KiB, or one 64 KiB chunk
-// of a larger block).  The input is staged in LDS with the 2048-entry u16
-// hash table (snappy.c:25,107).  The greedy parse is serial by definition;
-// the wave makes it cheap instead of parallel-but-different:
+// of a larger block).  The chunk is staged in LDS at address 0, the
+// 2048-entry u16 hash table (snappy.c:25,107) right after it at a constant
+// offset that the table's LDS instructions carry in their offset field.  The
+// greedy parse is serial by definition; the wave makes each serial step
+// cheap instead of parallel-but-different:
 //
-//  * literal search: the probe positions of snappy.c:138-143 depend only on
+//  * search batches: the probe positions of snappy.c:138-143 depend only on
 //    the probe's index k since the search started (skip = 32, += skip >> 5),
-//    so 64 lanes take probes k..k+63 at once.  Each lane hashes its position
-//    and reads its candidate from the table as it stood before the batch.
-//    That is exact for every lane whose hash no earlier lane of the batch
-//    shares; a lane-id scatter/gather through LDS finds the first lane that
-//    collides and the batch is cut there (lanes before it are all exact,
-//    lane 0 always is).  The first lane whose 4-byte compare matches ends the
-//    search; table writes of the lanes up to it are committed, later lanes
-//    are discarded -- exactly the state the serial loop would leave.
-//  * match extension (snappy.c:163-164): 64 byte-compares per step, the
-//    first mismatch found by ballot.
-//  * post-copy re-probe, including lcdb's 64-bit compare (snappy.c:172-186):
-//    the same work on every lane (VALU + LDS broadcast), off the scalar unit.
-//  * emission (snappy.c:53-102): the literal and the copy tags that follow it
-//    in one lane-parallel pass, stored straight to the output.
+//    so lanes 2..63 take 62 probes at once; lanes 0-1 are the re-probe after
+//    a copy (snappy.c:172-186: A at at-1, B at at with lcdb's 64-bit compare
+//    of :182), off in a batch that does not follow a copy.  Each lane swaps
+//    its position into its hash's u16 entry with one ds_mskor_rtn_b32; lanes
+//    of one instruction that hit the same dword apply in lane order, so each
+//    lane receives the entry the serial loop would read and the table ends as
+//    the serial loop leaves it.  The first matching lane ends the search;
+//    lanes after it store back what they received.  A lane receiving a later
+//    position than its own would mean the order broke: the batch then undoes
+//    its swaps and replays lane by lane (never seen on gfx950).
+//  * one path per round: the loop is rotated so a batch is its only exit
+//    test, and lane validity is recomputed per batch rather than carried
+//    (a carried bool becomes a lane-mask phi merged with exec on every path).
+//  * match extension (snappy.c:163-164): 64 byte compares per step, the
+//    first mismatch found by ballot.  (Sizing copies shorter than 8 bytes
+//    from an 8-byte candidate compare in the batch was measured 3 % slower:
+//    the third dword read sits on every batch's critical path.)
+//  * emission (snappy.c:53-102): each op is recorded in lane k of two VGPRs;
+//    every 64 ops flush_ops writes the literals and copy tags lane-parallel,
+//    a wave scan placing them, straight to the output slot.
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
@@ -534,9 +542,8 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
   uint32_t p;
   uint64_t vmask = 0;
   Raw64 xr;
-  // The batch's table state, kept for the copy that follows a match, and
-  // each lane's bytes 4..7 of probe against candidate (0: they match).
-  uint32_t prev = 0, h2 = 0, ta = 0, sh = 0, mask = 0, d47 = 0;
+  // The batch's table state, kept for the copy that follows a match.
+  uint32_t prev = 0, h2 = 0, ta = 0, sh = 0, mask = 0;
   // ---- one batch: snappy.c:146-152 for its 64 probes, `valid` the lanes
   // that are probes.  Returns the lanes that match.  (Validity is passed in,
   // not kept: a bool carried around the loop becomes a lane-mask phi merged
@@ -558,7 +565,7 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     mask = 0xffffu << sh;
     const uint32_t old = lds_mskor_rtn<TAB>(ta, mask, p << sh);   // snappy.c:146-148
     prev = (old >> sh) & 0xffffu;
-    Raw64 yr = x.raw64(prev);                                     // the candidate's bytes
+    Raw32 yr = x.raw32(prev);                                     // the candidate's bytes
     // (Checked under the read's latency; the rare path reads them again.)
 #ifdef LGS_PROBE_FORCE_REPLAY
     // Probe build (tools/probe_ab.py): every batch takes the replay path, so
@@ -577,18 +584,13 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
         const uint32_t got = lds_mskor_rtn<TAB>(lane == l ? ta : kSinkOff, mask, p << sh);
         prev = lane == l ? (got >> sh) & 0xffffu : prev;
       }
-      yr = x.raw64(prev);
+      yr = x.raw32(prev);
     }
-    uint32_t yv = yr.lo(), yh = yr.hi();
+    uint32_t yv = yr.value();
     if constexpr (IN::kWin) {
-      const bool o8 = valid & x.oow(prev, 8);
-      if (ballot(o8)) {
-        const uint64_t g = x.g64(prev);
-        yv = o8 ? (uint32_t)g : yv;
-        yh = o8 ? (uint32_t)(g >> 32) : yh;
-      }
+      const bool o4 = valid & x.oow(prev, 4);
+      if (ballot(o4)) yv = o4 ? x.g32(prev) : yv;
     }
-    d47 = xh ^ yh;
     // snappy.c:152; lane B: lcdb's 64-bit compare (snappy.c:182), bytes
     // at..at+6 against a zero-extended 4-byte load; A never matches.
     return ballot(((xv ^ yv) | (xh & pl.bm)) == 0) & vmask & ~1ull;
@@ -620,14 +622,9 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
                                    (((lane > m) & (prev <= base)) ? (ta | (h2 & 2u)) : kSinkOff)) =
           (uint16_t)prev;
       const uint32_t dist = base - ref;
-      // Bytes 4..7 were compared in the batch (the candidate's read took
-      // its third dword): a copy shorter than 8 bytes ends there, with no
-      // extension round trip.  (Probe and candidate both lie at least 15
-      // bytes before the chunk's end, snappy.c:106, so all 8 are inside.)
-      const uint32_t e47 = lane_val(d47, m);
-      uint32_t at_n = base + 4 + (e47 ? (uint32_t)__builtin_ctz(e47) >> 3 : 4u);
+      uint32_t at_n = base + 4;
 #pragma clang loop unroll(disable)
-      for (; !e47;) {                                             // snappy.c:163-164
+      for (;;) {                                                  // snappy.c:163-164
         const uint32_t q = at_n + lane;
         if constexpr (IN::kWin) x.ensure(at_n + kWave);
         // Unconditional reads, unclamped: lanes at q >= n read at most 63
