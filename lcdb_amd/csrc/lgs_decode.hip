@@ -958,6 +958,9 @@ constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoo
 // batch).  On incompressible blocks the wave kernel wins at every size
 // (98 against 163 us at 49 152), but a launch does not know the ratio.
 constexpr uint32_t kLaneMinBlocks = 36864;
+// Batches of at most this many blocks go to the workgroup-per-block decoder
+// (one block per CU at a time).
+constexpr uint32_t kGroupMaxBlocks = 32;
 
 // ---------------------------------------------------------------------------
 // Mixed-size batches.  One launch sized for its largest block runs every
@@ -1044,11 +1047,16 @@ static hipError_t launch_decode_wide(const DecodeArgs& a, hipStream_t s) {
 }
 // The wide class: the one-tag walk (a probe build can select the trip
 // decoder of lgs_decode_probe.hip).
-static hipError_t launch_decode_big(const DecodeArgs& a, hipStream_t s) {
+// max_out: the largest capacity the launch may hold (the workgroup decoder
+// takes the 64 KiB class, never larger outputs).
+static hipError_t launch_decode_big(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
 #ifdef LGS_PROBE_DECODERS
   if (options().wide.load(std::memory_order_relaxed) == kWideTrips)
     return launch_decode_trips(a, s);
 #endif
+  if (max_out <= kGroupMaxOut && (options().wide.load(std::memory_order_relaxed) == kWideGroup ||
+                                  options().decoder.load(std::memory_order_relaxed) == kDecGroup))
+    return launch_decode_group(a, max_out, s);
   return launch_decode_wide<32768, 4096>(a, s);
 }
 // The 16 KiB class stays in decode_kernel's in-place image (18 KB, eight
@@ -1078,11 +1086,11 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
   LGS_TRY(launch_decode_mid(c, s));
   if (max_out > kDecCap1) {            // (classes above max_out are empty)
     c.index = list + 2 * (size_t)a.n; c.count = cnt + 2;
-    LGS_TRY(launch_decode_big(c, s));
+    LGS_TRY(launch_decode_big(c, kDecCap2, s));
   }
   if (max_out > kDecCap2) {
     c.index = list + 3 * (size_t)a.n; c.count = cnt + 3;
-    LGS_TRY(launch_decode_big(c, s));
+    LGS_TRY(launch_decode_big(c, max_out, s));
   }
   return scratch.release();
 }
@@ -1099,9 +1107,14 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
     return launch_decode_split(a, max_out, s);
   if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))
     return launch_decode_ring(a, s);
+  // A few blocks leave the chip idle under a wave or a lane per block: a
+  // workgroup per block walks none of the tag chain serially.
+  if ((force == kDecGroup || (force == kDecAuto && a.n <= kGroupMaxBlocks)) &&
+      max_out <= kGroupMaxOut)
+    return launch_decode_group(a, max_out, s);
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_mid(a, s);
-  return launch_decode_big(a, s);
+  return launch_decode_big(a, max_out, s);
 }
 
 }  // namespace lgs

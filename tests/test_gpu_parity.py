@@ -208,7 +208,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops"]))
+@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring", "group"], ["quad", "ops"]))
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -227,7 +227,7 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops")]))
+@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave", "group")], [("quad", "ops")]))
 def test_decode_kernels_c2_full_size(gpu, digests, force, kernels):
     import torch
     from lcdb_amd import batch
@@ -379,7 +379,7 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops"]))
+@pytest.mark.parametrize("kernel", _with_probe(["ring", "group"], ["quad", "ops"]))
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
@@ -512,7 +512,7 @@ if PROBE:   # the two-pass decoder exists in the probe library only
 
 
 
-@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops"]))
+@pytest.mark.parametrize("kernel", _with_probe([None, "ring", "group"], ["quad", "ops"]))
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
@@ -711,7 +711,7 @@ def _trip_stress_stream(rng, want: int) -> bytes:
     return _varint(len(out)) + bytes(s), bytes(out)
 
 
-@pytest.mark.parametrize("wide", _with_probe(["walk"], ["trips"]))
+@pytest.mark.parametrize("wide", _with_probe(["walk", "group"], ["trips"]))
 def test_decode_wide_dependent_copies_and_c3(gpu, digests, force, wide):
     # The wide class (outputs over 16 KiB) on C3 (its 64 KiB fillseq and
     # random classes among the others) and on hand-made streams dense in
@@ -750,3 +750,89 @@ def test_decode_wide_dependent_copies_and_c3(gpu, digests, force, wide):
             assert code == gpu.LGS_ST_CORRUPT, k
         else:
             assert code == gpu.LGS_ST_OK and o == exp, k
+
+
+def _group_streams(rng, ref):
+    """Streams for the workgroup decoder's windows (4 096 stream bytes,
+    8 192 output bytes each): real 4 / 16 / 64 KiB blocks, dependent-copy
+    stress streams, long literals crossing windows, outputs that cut windows
+    (64-byte copies of dist 1: 21 output bytes per stream byte), every reject
+    placed in the first, a middle and the last window, and their corruptions."""
+    streams = []
+    for c in (corpus.fillseq(6), corpus.fillseq(3, 16384, key0=9), corpus.fillseq(3, 65536, key0=3),
+              corpus.random_blocks(3, 4096), corpus.random_blocks(2, 65536, seed=9)):
+        for b in c.blocks():
+            s = ref.encode(b)
+            streams += [s, s[:-1], s[:-5]]
+            for _ in range(6):
+                k = rng.randrange(len(s))
+                streams.append(s[:k] + bytes([rng.randrange(256)]) + s[k + 1:])
+    for want in (100, 4000, 9000, 16000, 40000, 66000):
+        for _ in range(3):
+            s, _o = _trip_stress_stream(rng, want)
+            streams += [s, s[:-1]]
+            k = rng.randrange(1, len(s))
+            streams.append(s[:k] + bytes([rng.randrange(256)]) + s[k + 1:])
+    rnd = lambda n: bytes(rng.randrange(256) for _ in range(n))  # noqa: E731
+    # runs: one literal, then 64-byte copies of dist 1 (window output cut)
+    for want in (9000, 30000, 66000):
+        n = (want - 1) // 64
+        body = _lit(b"z") + _copy2(64, 1) * n + _lit(b"q" * (want - 1 - 64 * n))
+        streams += [_varint(want) + body, _varint(want + 1) + body, _varint(want - 1) + body]
+    # long literals straddling windows, between copies
+    for n in (4090, 4100, 8191, 8192, 8193, 20000, 65000):
+        lit = rnd(n)
+        body = _lit(lit[:10]) + _copy2(8, 10) + _lit(lit) + _copy2(64, n // 2 + 1) + _lit(b"end")
+        want = 10 + 8 + n + 64 + 3
+        if want <= 66048:
+            streams += [_varint(want) + body, _varint(want) + body[:-2]]
+    # rejects in the first / a middle / the last window
+    base = _lit(rnd(3000)) + _copy2(60, 2900) * 40 + _lit(rnd(100))
+    made = 3000 + 60 * 40 + 100
+    for bad in (bytes([2, 0, 0]),                          # dist 0
+                _copy2(64, 60000),                         # dist > made
+                bytes([(63 << 2) | 3]) + (2**31).to_bytes(4, "little"),   # dist >= 2^31
+                bytes([63 << 2]) + b"\xff\xff\xff\x7f",    # literal length 2^31
+                bytes([62 << 2, 0xff, 0xff]),              # header past the stream
+                _copy2(64, 1)):                            # past want
+        for pre in (b"", base, base * 3):
+            pm = made * (len(pre) // len(base)) if pre else 0
+            streams.append(_varint(pm + 4) + pre + bad + _lit(b"tail"))
+    streams += [b"", b"\x00", b"\x80", b"\x00\x00", b"\x01\x00a", b"\x05\x10abcd",
+                _varint(3) + _lit(b"ab") + bytes([1, 1]), _varint(0) + _lit(b"x")]
+    return streams
+
+
+@pytest.mark.parametrize("cap", [4608, 16896, 66048])
+def test_decode_group_windows_and_rejects(gpu, force, cap):
+    # The workgroup decoder forced on every stream of _group_streams, at each
+    # of its LDS classes, against the reference's bytes and accept/reject bit
+    # (a header beyond the capacity is LGS_ST_NOSPACE, as in every decoder).
+    import random
+    force("decoder", "group")
+    rng = random.Random(cap)
+    ref = oracle.best()
+    streams = _group_streams(rng, ref)
+    res, st = gpu.decode_batch_host(streams, [cap] * len(streams))
+    oks = 0
+    for k, (s, o, code) in enumerate(zip(streams, res, st)):
+        exp = ref.decode(s) if s else None
+        h = _header(s)
+        if h is not None and h > cap:
+            assert code == gpu.LGS_ST_NOSPACE, k
+        elif exp is None:
+            assert code == gpu.LGS_ST_CORRUPT, k
+        else:
+            assert code == gpu.LGS_ST_OK and o == exp, k
+            oks += 1
+    assert oks >= 20
+
+
+def test_decode_group_dropin_and_odd_outputs(gpu):
+    # Single blocks through the drop-in take the workgroup decoder (n = 1);
+    # outputs at every 16-byte phase exercise its head / tail granules.
+    import random
+    rng = random.Random(5)
+    ref = oracle.best()
+    for s in _group_streams(rng, ref)[:400]:
+        assert gpu.decode(s) == (ref.decode(s) if s else None)

@@ -1,9 +1,16 @@
 set -u
-bash tools/ab_run.sh > gpurun_out/r4f_ab.txt 2>&1; echo AB_EXIT $? >> gpurun_out/r4f_ab.txt
-PROBE_CHECK=1 timeout -k 10 300 python tools/probe_ab.py probes/new.so probes/fold.so probes/new.so probes/fold.so > gpurun_out/r4f_fold.txt 2>&1 || exit 1
-PROBE_CHECK=1 timeout -k 10 300 python tools/probe_ab.py probes/q0.so@quad probes/q1.so@quad probes/q2.so@quad > gpurun_out/r4f_quad.txt 2>&1 || exit 1
-NO_TDB=1 REPS=1000 timeout -k 10 300 python tools/bench_dropin_latency.py > gpurun_out/r4f_dropin.json 2>&1 || exit 1
-PASSES="sqA sqB" bash tools/profile.sh r4f_new --blocks 65536 --iters 2 --which encode --lib probes/new.so > /dev/null 2>&1 || exit 1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_probe_decoders.py -x -q -p no:cacheprovider --timeout 700 --timeout-method thread > gpurun_out/r4f_probe.txt 2>&1; echo PROBE_EXIT $? >> gpurun_out/r4f_probe.txt
-PROBE_CHECK=1 timeout -k 10 300 python tools/probe_ab.py probes/replay.so > gpurun_out/r4f_replay.txt 2>&1
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && NO_TDB=1 REPS=300 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r4f_dropin -o dropin --output-format csv -- python3 tools/bench_dropin_latency.py > gpurun_out/r4f_dropin_rocprof.txt 2>&1
+# round 4 session h: the workgroup decoder's parity, then its timings.
+T="python -u -m pytest -x -q -p no:cacheprovider --timeout 200 --timeout-method thread"
+timeout -k 10 400 $T tests/test_gpu_parity.py -k "group" > gpurun_out/r4h_group.txt 2>&1 || { tail -30 gpurun_out/r4h_group.txt; exit 1; }
+tail -2 gpurun_out/r4h_group.txt
+timeout -k 10 500 $T tests/test_gpu_parity.py tests/test_dropin_contract.py > gpurun_out/r4h_parity.txt 2>&1 || { tail -30 gpurun_out/r4h_parity.txt; exit 1; }
+tail -2 gpurun_out/r4h_parity.txt
+NO_TDB=1 REPS=1000 timeout -k 10 300 python tools/bench_dropin_latency.py > gpurun_out/r4h_dropin.json 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_mixed.py --iters 10 > gpurun_out/r4h_mixed_walk.json 2>&1 || exit 1
+LGS_WIDE_DECODER=group timeout -k 10 300 python tools/bench_mixed.py --iters 10 > gpurun_out/r4h_mixed_group.json 2>&1 || exit 1
+LGS_DECODE_KERNEL=quad timeout -k 10 200 python tools/quad_diag.py probes/q1.so 6 > gpurun_out/r4h_quad_diag.txt 2>&1
+for f in r4h_mixed_walk r4h_mixed_group; do python -c "
+import json; d=json.load(open('gpurun_out/$f.json'))
+print('$f', {k:(round(v['encode_GiBps'],1), round(v['decode_GiBps'],1)) for k,v in d['classes'].items()}, 'mix', round(d['mixed_one_launch']['encode_GiBps'],1), round(d['mixed_one_launch']['decode_GiBps'],1), d['parity'])"; done
+tail -c 400 gpurun_out/r4h_dropin.json; echo
+grep -v amdgpu.ids gpurun_out/r4h_quad_diag.txt | head -8
