@@ -798,7 +798,13 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   // Rotated: the loop's test is its last step (a test at the top became a
   // selector variable and a bool round trip through a VGPR).  A trip with no
   // active lane (every block's header corrupt) does nothing.
+#ifdef LGS_PROBE_TRIPCOUNT
+  uint32_t trips = 0;   // probe build (tools/ring_trips.py): trips of this wave
+#endif
   do {
+#ifdef LGS_PROBE_TRIPCOUNT
+    ++trips;
+#endif
 
     // ---- one piece of the current op for every lane whose bytes are in LDS;
     // this runs before the wait, so last trip's loads land meanwhile.
@@ -926,7 +932,11 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
 
   if (exists) {
     status[i] = (uint8_t)st;
+#ifdef LGS_PROBE_TRIPCOUNT
+    out_len[i] = trips;
+#else
     out_len[i] = st == 1 ? want : 0;
+#endif
   }
 }
 

@@ -318,10 +318,22 @@ __global__ __launch_bounds__(NT) void decode_group_kernel(
         if (r0 != wo + o) s.img[sh + wo + o] = s.img[sh + r0];
       }
     } else {
+      // A literal longer than OUT_WIN alone: straight from the stream in
+      // 16-byte granules of the image (aligned LDS writes); the granules at
+      // either end only take their own bytes (the first holds earlier
+      // output).  Loads may run 15 bytes past the literal, inside the stream
+      // or its read slack.
       const uint32_t lp = s.os[0];
-      for (uint32_t o = t; o < wl; o += NT) {
-        const uint32_t q = lp + o;
-        s.img[sh + wo + o] = q - ws < L::kSw ? s.sw[q - ws] : src[q];
+      const uint32_t i0 = sh + wo, i1 = i0 + wl;          // image range
+      for (uint32_t g = (i0 & ~15u) + 16 * t; g < i1; g += 16 * NT) {
+        const int32_t d = (int32_t)g - (int32_t)i0;        // literal offset of byte g
+        if ((d >= 0) & (g + 16 <= i1)) {
+          lwr16(s.img + g, ld16(src + lp + (uint32_t)d));
+        } else {
+#pragma unroll 1
+          for (uint32_t b = g; b < g + 16; ++b)
+            if ((b >= i0) & (b < i1)) s.img[b] = src[lp + (b - i0)];
+        }
       }
     }
     __syncthreads();

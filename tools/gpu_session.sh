@@ -8,9 +8,18 @@ tail -2 gpurun_out/r4h_parity.txt
 NO_TDB=1 REPS=1000 timeout -k 10 300 python tools/bench_dropin_latency.py > gpurun_out/r4h_dropin.json 2>&1 || exit 1
 timeout -k 10 300 python tools/bench_mixed.py --iters 10 > gpurun_out/r4h_mixed_walk.json 2>&1 || exit 1
 LGS_WIDE_DECODER=group timeout -k 10 300 python tools/bench_mixed.py --iters 10 > gpurun_out/r4h_mixed_group.json 2>&1 || exit 1
+timeout -k 10 200 python tools/pipe_ab.py 20 > gpurun_out/r4h_pipe.txt 2>&1 || exit 1
 LGS_DECODE_KERNEL=quad timeout -k 10 200 python tools/quad_diag.py probes/q1.so 6 > gpurun_out/r4h_quad_diag.txt 2>&1
 for f in r4h_mixed_walk r4h_mixed_group; do python -c "
 import json; d=json.load(open('gpurun_out/$f.json'))
 print('$f', {k:(round(v['encode_GiBps'],1), round(v['decode_GiBps'],1)) for k,v in d['classes'].items()}, 'mix', round(d['mixed_one_launch']['encode_GiBps'],1), round(d['mixed_one_launch']['decode_GiBps'],1), d['parity'])"; done
 tail -c 400 gpurun_out/r4h_dropin.json; echo
 grep -v amdgpu.ids gpurun_out/r4h_quad_diag.txt | head -8
+grep -v amdgpu.ids gpurun_out/r4h_pipe.txt
+timeout -k 10 120 python tools/ring_trips.py probes/tripcount.so > gpurun_out/r4h_trips.json 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/r4h_trips.json
+PASSES="sqA sqB fetch write" bash tools/profile.sh r4h_ring --blocks 65536 --iters 2 --which decode > /dev/null 2>&1 || exit 1
+PASSES="fetch" bash tools/profile.sh r4h_refill --blocks 65536 --iters 2 --which decode --lib probes/nofarflush.so > /dev/null 2>&1 || exit 1
+python tools/pmc_summary.py gpurun_out/prof_r4h_ring > gpurun_out/r4h_ring_pmc.txt 2>&1
+python tools/pmc_summary.py gpurun_out/prof_r4h_refill > gpurun_out/r4h_refill_pmc.txt 2>&1
+tail -5 gpurun_out/r4h_ring_pmc.txt gpurun_out/r4h_refill_pmc.txt
