@@ -607,9 +607,15 @@ constexpr uint32_t kInSink = kInRing + 64;             // a lane's sink slot (it
 __device__ __forceinline__ void out_put(uint8_t* ob, uint32_t p, u32x4 v) {
   const uint32_t r = p & (ring::kOutRing - 1);
   lwr16(ob + r, v);
+#ifdef LGS_PROBE_RING_SINKMIRROR
+  // Every lane writes a second copy: the mirror / wrapped part, or the 16
+  // bytes after its mirror (the stride's tail pad) -- no exec-mask region.
+  lwr16(ob + (r < 64 ? (int32_t)r + 256 : (r > 240 ? (int32_t)r - 256 : 320)), v);
+#else
   // r < 64 or r > 240 as one unsigned compare; the second copy's offset as
   // one select (its value for the other lanes is never used).
   if (r - 64 > 176u) lwr16(ob + (int32_t)r + (r < 64 ? 256 : -256), v);
+#endif
 }
 
 // A cooperative job (a refill or a flush) of one lane, 16 bytes: the lane
@@ -743,6 +749,15 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           const uint32_t py = dist == 8 ? c0.y : px;
           const u32x4 pv = {px, py, px, py};
           out_put(ob, made, pat ? pv : c0);
+#ifdef LGS_PROBE_RING_PATSRC
+          // A pattern's later chunks repeat chunk 0: read back the chunk just
+          // written (LDS program order) instead of selecting 16 dwords.
+          const uint8_t* sq = pat ? ob + (made & (kOutRing - 1)) : sp;
+          const uint32_t sd = pat ? 0u : 16u;
+          if (piece > 16) out_put(ob, made + 16, lrd16(sq + sd));
+          if (piece > 32) out_put(ob, made + 32, lrd16(sq + 2 * sd));
+          if (piece > 48) out_put(ob, made + 48, lrd16(sq + 3 * sd));
+#else
           // Later chunks are read only when the piece has them (and not for
           // a pattern).  A source chunk can share ring slots only with a
           // later destination chunk (dist <= 240), so reading chunk k just
@@ -750,6 +765,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           if (piece > 16) out_put(ob, made + 16, pat ? pv : lrd16(sp + 16));
           if (piece > 32) out_put(ob, made + 32, pat ? pv : lrd16(sp + 32));
           if (piece > 48) out_put(ob, made + 48, pat ? pv : lrd16(sp + 48));
+#endif
         }
         made += piece;
         orem -= piece;

@@ -161,29 +161,36 @@ __global__ __launch_bounds__(NT) void decode_group_kernel(
   }
   uint32_t st = (hlen == 0 || want > 0x7fffffffu) ? 0u : (want > cap ? 2u : 1u);
 
-  uint32_t ws = hlen, wo = 0;                 // window start (stream), output made
-  uint32_t F = sh ? 16u : 0u;                 // image offset flushed up to (granules)
-  while ((st == 1) & (ws < S)) {               // snappy.c:208
-    const uint32_t wn = S - ws < IN_WIN ? S - ws : IN_WIN;
-    const uint32_t avail = S - ws;
-    // ---- 1. stage the window (reads stay within 15 bytes past the stream)
-    for (uint32_t g = t; g < L::kSw / 16; g += NT) {
-      const uint32_t o = 16 * g;
-      u32x4 v = {0, 0, 0, 0};
-      if (o < avail) {
-        v = ld16(src + ws + o);
-        if (avail - o < 16) {
-          const uint32_t k = avail - o;      // bytes 0..k-1 are the stream's
+  // One 16-byte granule of the window that starts at stream offset `base`
+  // (thread t's; zero past the stream; loads stay within 15 bytes past it).
+  static_assert(L::kSw / 16 <= NT, "one staging granule per thread");
+  auto fetch = [&](uint32_t base) -> u32x4 {
+    u32x4 v = {0, 0, 0, 0};
+    const uint32_t o = 16 * t;
+    if ((t < L::kSw / 16) & (base < S) && o < S - base) {
+      v = ld16(src + base + o);
+      const uint32_t k = S - base - o;        // bytes 0..k-1 are the stream's
+      if (k < 16) {
 #pragma unroll
-          for (uint32_t d = 0; d < 4; ++d) {
-            const uint32_t lo = 4 * d;
-            const uint32_t keep = k <= lo ? 0u : (k >= lo + 4 ? 0xffffffffu : (1u << (8 * (k - lo))) - 1u);
-            v[d] &= keep;
-          }
+        for (uint32_t d = 0; d < 4; ++d) {
+          const uint32_t lo = 4 * d;
+          const uint32_t keep = k <= lo ? 0u : (k >= lo + 4 ? 0xffffffffu : (1u << (8 * (k - lo))) - 1u);
+          v[d] &= keep;
         }
       }
-      lwr16(s.sw + o, v);
     }
+    return v;
+  };
+
+  uint32_t ws = hlen, wo = 0;                 // window start (stream), output made
+  uint32_t F = sh ? 16u : 0u;                 // image offset flushed up to (granules)
+  // The next window's granule, loaded while the current one decodes (its
+  // start is known once the current window's ops are placed).
+  u32x4 pf = fetch(ws);
+  while ((st == 1) & (ws < S)) {               // snappy.c:208
+    const uint32_t wn = S - ws < IN_WIN ? S - ws : IN_WIN;
+    // ---- 1. stage the window
+    if (t < L::kSw / 16) lwr16(s.sw + 16 * t, pf);
     __syncthreads();
     // ---- 2. parse every position (stream-only rejects: made/want checks off)
 #pragma unroll
@@ -273,6 +280,7 @@ __global__ __launch_bounds__(NT) void decode_group_kernel(
       wl = s.oo[1];
       nws = nops > 1 ? ws + (s.opos[1] & 0x7fffu) : s.ctl[kNext];
     }
+    pf = fetch(nws);
     // ---- 5-6. literal bytes and copy sources; resolve; gather
     if (!solo) {
       uint32_t k = scan_max<NT>(s.cov[t], s.red);

@@ -5,7 +5,10 @@ timeout -k 10 400 $T tests/test_gpu_parity.py -k "group" > gpurun_out/r4h_group.
 tail -2 gpurun_out/r4h_group.txt
 timeout -k 10 500 $T tests/test_gpu_parity.py tests/test_dropin_contract.py > gpurun_out/r4h_parity.txt 2>&1 || { tail -30 gpurun_out/r4h_parity.txt; exit 1; }
 tail -2 gpurun_out/r4h_parity.txt
+PROBE_CHECK=1 timeout -k 10 400 python tools/probe_ab.py probes/cur.so probes/patsrc.so probes/sinkmirror.so probes/both.so probes/cur.so probes/patsrc.so > gpurun_out/r4h_ring_ab.txt 2>&1 || exit 1
+grep -v amdgpu.ids gpurun_out/r4h_ring_ab.txt
 NO_TDB=1 REPS=1000 timeout -k 10 300 python tools/bench_dropin_latency.py > gpurun_out/r4h_dropin.json 2>&1 || exit 1
+REPS=300 timeout -k 10 200 python tools/dropin_breakdown.py > gpurun_out/r4h_breakdown.json 2>&1 || exit 1
 timeout -k 10 300 python tools/bench_mixed.py --iters 10 > gpurun_out/r4h_mixed_walk.json 2>&1 || exit 1
 LGS_WIDE_DECODER=group timeout -k 10 300 python tools/bench_mixed.py --iters 10 > gpurun_out/r4h_mixed_group.json 2>&1 || exit 1
 timeout -k 10 200 python tools/pipe_ab.py 20 > gpurun_out/r4h_pipe.txt 2>&1 || exit 1
@@ -14,6 +17,7 @@ for f in r4h_mixed_walk r4h_mixed_group; do python -c "
 import json; d=json.load(open('gpurun_out/$f.json'))
 print('$f', {k:(round(v['encode_GiBps'],1), round(v['decode_GiBps'],1)) for k,v in d['classes'].items()}, 'mix', round(d['mixed_one_launch']['encode_GiBps'],1), round(d['mixed_one_launch']['decode_GiBps'],1), d['parity'])"; done
 tail -c 400 gpurun_out/r4h_dropin.json; echo
+grep -v amdgpu.ids gpurun_out/r4h_breakdown.json
 grep -v amdgpu.ids gpurun_out/r4h_quad_diag.txt | head -8
 grep -v amdgpu.ids gpurun_out/r4h_pipe.txt
 timeout -k 10 120 python tools/ring_trips.py probes/tripcount.so > gpurun_out/r4h_trips.json 2>&1 || exit 1
