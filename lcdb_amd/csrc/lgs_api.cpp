@@ -727,10 +727,11 @@ Options& options_init() {
     const char* dk = getenv("LGS_DECODE_KERNEL");
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
+    if (dk && !strcmp(dk, "chain")) v->decoder = kDecChain;
+#ifdef LGS_PROBE_DECODERS
     if (dk && !strcmp(dk, "group")) v->decoder = kDecGroup;
     const char* wg = getenv("LGS_WIDE_DECODER");
     if (wg && !strcmp(wg, "group")) v->wide = kWideGroup;
-#ifdef LGS_PROBE_DECODERS
     if (dk && !strcmp(dk, "quad")) v->decoder = kDecQuad;
     if (dk && !strcmp(dk, "ops")) v->decoder = kDecOps;
     const char* wd = getenv("LGS_WIDE_DECODER");
@@ -809,14 +810,15 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
-    else if (!strcmp(value, "group")) o.decoder = kDecGroup;
+    else if (!strcmp(value, "chain")) o.decoder = kDecChain;
 #ifdef LGS_PROBE_DECODERS
+    else if (!strcmp(value, "group")) o.decoder = kDecGroup;
     // The decoders that lost their A/B exist in the probe library only
     // (lgs_decode_probe.hip); the product rejects them.
     else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
     else if (!strcmp(value, "ops")) o.decoder = kDecOps;
 #endif
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring, wave or group)", value);
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring, wave or chain)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)
@@ -829,11 +831,11 @@ int lgs_set_option(const char* name, const char* value) {
   }
   if (!strcmp(name, "wide")) {
     if (!strcmp(value, "walk") || !*value) o.wide = kWideWalk;
-    else if (!strcmp(value, "group")) o.wide = kWideGroup;
 #ifdef LGS_PROBE_DECODERS
+    else if (!strcmp(value, "group")) o.wide = kWideGroup;
     else if (!strcmp(value, "trips")) o.wide = kWideTrips;
 #endif
-    else return fail(LGS_EINVAL, "wide '%s' (walk or group)", value);
+    else return fail(LGS_EINVAL, "wide '%s' (walk)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "split")) {

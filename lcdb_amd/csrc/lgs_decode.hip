@@ -607,15 +607,12 @@ constexpr uint32_t kInSink = kInRing + 64;             // a lane's sink slot (it
 __device__ __forceinline__ void out_put(uint8_t* ob, uint32_t p, u32x4 v) {
   const uint32_t r = p & (ring::kOutRing - 1);
   lwr16(ob + r, v);
-#ifdef LGS_PROBE_RING_SINKMIRROR
-  // Every lane writes a second copy: the mirror / wrapped part, or the 16
-  // bytes after its mirror (the stride's tail pad) -- no exec-mask region.
-  lwr16(ob + (r < 64 ? (int32_t)r + 256 : (r > 240 ? (int32_t)r - 256 : 320)), v);
-#else
   // r < 64 or r > 240 as one unsigned compare; the second copy's offset as
-  // one select (its value for the other lanes is never used).
+  // one select (its value for the other lanes is never used).  (Written by
+  // every lane, to a pad for the others, it cost 1.5 %; the whole trip
+  // branch-free that way, 35 %: LDS stores cost by the lanes they move,
+  // profiles/r4h_session.txt.)
   if (r - 64 > 176u) lwr16(ob + (int32_t)r + (r < 64 ? 256 : -256), v);
-#endif
 }
 
 // A cooperative job (a refill or a flush) of one lane, 16 bytes: the lane
@@ -749,15 +746,6 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           const uint32_t py = dist == 8 ? c0.y : px;
           const u32x4 pv = {px, py, px, py};
           out_put(ob, made, pat ? pv : c0);
-#ifdef LGS_PROBE_RING_PATSRC
-          // A pattern's later chunks repeat chunk 0: read back the chunk just
-          // written (LDS program order) instead of selecting 16 dwords.
-          const uint8_t* sq = pat ? ob + (made & (kOutRing - 1)) : sp;
-          const uint32_t sd = pat ? 0u : 16u;
-          if (piece > 16) out_put(ob, made + 16, lrd16(sq + sd));
-          if (piece > 32) out_put(ob, made + 32, lrd16(sq + 2 * sd));
-          if (piece > 48) out_put(ob, made + 48, lrd16(sq + 3 * sd));
-#else
           // Later chunks are read only when the piece has them (and not for
           // a pattern).  A source chunk can share ring slots only with a
           // later destination chunk (dist <= 240), so reading chunk k just
@@ -765,7 +753,6 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           if (piece > 16) out_put(ob, made + 16, pat ? pv : lrd16(sp + 16));
           if (piece > 32) out_put(ob, made + 32, pat ? pv : lrd16(sp + 32));
           if (piece > 48) out_put(ob, made + 48, pat ? pv : lrd16(sp + 48));
-#endif
         }
         made += piece;
         orem -= piece;
@@ -773,6 +760,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       }
     }
   };
+
 
   // Parse the next tag (its bytes are in the window); a far copy's bytes are
   // loaded from the flushed output for the next trip.
@@ -984,9 +972,9 @@ constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoo
 // batch).  On incompressible blocks the wave kernel wins at every size
 // (98 against 163 us at 49 152), but a launch does not know the ratio.
 constexpr uint32_t kLaneMinBlocks = 36864;
-// Batches of at most this many blocks go to the workgroup-per-block decoder
-// (one block per CU at a time).
-constexpr uint32_t kGroupMaxBlocks = 32;
+// Batches of at most this many blocks go to the chain decoder (the tag walk
+// apart from the byte moves: latency-bound single blocks).
+constexpr uint32_t kChainMaxBlocks = 32;
 
 // ---------------------------------------------------------------------------
 // Mixed-size batches.  One launch sized for its largest block runs every
@@ -1073,16 +1061,19 @@ static hipError_t launch_decode_wide(const DecodeArgs& a, hipStream_t s) {
 }
 // The wide class: the one-tag walk (a probe build can select the trip
 // decoder of lgs_decode_probe.hip).
-// max_out: the largest capacity the launch may hold (the workgroup decoder
-// takes the 64 KiB class, never larger outputs).
+// max_out: the largest capacity the launch may hold (the probe library's
+// workgroup decoder takes the 64 KiB class, never larger outputs).
 static hipError_t launch_decode_big(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
+  (void)max_out;
 #ifdef LGS_PROBE_DECODERS
   if (options().wide.load(std::memory_order_relaxed) == kWideTrips)
     return launch_decode_trips(a, s);
 #endif
+#ifdef LGS_PROBE_DECODERS
   if (max_out <= kGroupMaxOut && (options().wide.load(std::memory_order_relaxed) == kWideGroup ||
                                   options().decoder.load(std::memory_order_relaxed) == kDecGroup))
     return launch_decode_group(a, max_out, s);
+#endif
   return launch_decode_wide<32768, 4096>(a, s);
 }
 // The 16 KiB class stays in decode_kernel's in-place image (18 KB, eight
@@ -1133,11 +1124,14 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
     return launch_decode_split(a, max_out, s);
   if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))
     return launch_decode_ring(a, s);
-  // A few blocks leave the chip idle under a wave or a lane per block: a
-  // workgroup per block walks none of the tag chain serially.
-  if ((force == kDecGroup || (force == kDecAuto && a.n <= kGroupMaxBlocks)) &&
-      max_out <= kGroupMaxOut)
-    return launch_decode_group(a, max_out, s);
+#ifdef LGS_PROBE_DECODERS
+  if (force == kDecGroup && max_out <= kGroupMaxOut) return launch_decode_group(a, max_out, s);
+#endif
+  // A few blocks: each one's serial tag chain is the launch's latency, so
+  // the chain decoder walks it apart from the byte moves.
+  if ((force == kDecChain || (force == kDecAuto && a.n <= kChainMaxBlocks)) &&
+      max_out <= kChainMaxOut)
+    return launch_decode_chain(a, max_out, s);
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_mid(a, s);
   return launch_decode_big(a, max_out, s);

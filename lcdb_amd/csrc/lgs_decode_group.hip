@@ -1,7 +1,11 @@
 // lgs_decode_group.hip -- workgroup-per-block Snappy decoder for gfx950
-// (MI355X): the batches where the lane- and wave-per-block decoders leave the
-// chip idle -- the drop-in's single blocks, small batches, and the 64 KiB
-// class (C3: 1 024 blocks, one serial walk per SIMD).
+// (MI355X), PROBE LIBRARY ONLY (-DLGS_PROBE_DECODERS; tests/test_gpu_probe_
+// decoders.py).  Built for the batches where the lane- and wave-per-block
+// decoders leave the chip idle (single blocks, the 64 KiB class); exact, but
+// it loses: pointer jumping moves every stream position and output byte
+// through LDS ~15 times, and the CU's LDS is the bound -- 32 us for one
+// 4 KiB block against the wave decoder's 28, C3 fillseq 64 KiB 44 against
+// 144 GiB/s (profiles/r4h_session.txt).
 //
 // Semantics: lcdb src/util/snappy.c:386-412 and decode_blocks (:201-341);
 // every reject of :216-338 and :337, so the per-block accept/reject bit and
@@ -31,6 +35,9 @@
 // produce more is cut after the last op that fits, and the next window
 // starts at the next tag (a single literal longer than OUT_WIN is copied
 // alone).  Windows follow each other until the stream ends.
+#ifndef LGS_PROBE_DECODERS
+#error "lgs_decode_group.hip is built into the probe library only (build.py build_probe)"
+#endif
 #include "lgs_device.h"
 #include "lgs_decode_common.h"
 #include "lgs_launch.h"

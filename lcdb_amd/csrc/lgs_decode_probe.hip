@@ -624,6 +624,9 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
     order();
 #if LGS_PROBE_QUAD_TOP_REFILL == 1
     refill();
+#ifdef LGS_PROBE_QUAD_REFILL_SYNC
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // probe: the refills complete here
+#endif
 #endif
 
     // ---- flush: whole 64-byte segments of the destination up to made, the
@@ -797,11 +800,35 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
     // issued now, landed at the start of the next trip.
     if (ballot(my_far)) {
       const gptr<const uint8_t> fp = (gptr<const uint8_t>)(dst + (my_far ? my_src : 0u));
+#ifdef LGS_PROBE_QUAD_FAR_WAIT
+      __builtin_amdgcn_s_waitcnt(0x0f70);    // probe: nothing in flight before them
+#endif
       if (my_far) {
+#ifdef LGS_PROBE_QUAD_FARBYPASS
+        // probe: agent-scope dword loads (never served from the CU's L1)
+        auto gl4 = [&](gptr<const uint8_t> q) {
+          const uintptr_t a = reinterpret_cast<uintptr_t>(q);
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+          const uint32_t sh8 = 8 * (uint32_t)(a & 3u);
+          uint32_t d[5];
+#pragma unroll
+          for (int k = 0; k < 5; ++k) d[k] = __hip_atomic_load(w + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          u32x4 v;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            v[k] = sh8 ? (d[k] >> sh8) | (d[k + 1] << (32 - sh8)) : d[k];
+          return v;
+        };
+        fv0 = gl4(fp);
+        fv1 = gl4(fp + 16);
+        fv2 = gl4(fp + 32);
+        fv3 = gl4(fp + 48);
+#else
         fv0 = ld16(fp);
         fv1 = ld16(fp + 16);
         fv2 = ld16(fp + 32);
         fv3 = ld16(fp + 48);
+#endif
       }
       fat = my_far ? my_at : fat;
       flen = my_far ? my_n : 0u;

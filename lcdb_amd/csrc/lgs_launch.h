@@ -14,10 +14,11 @@ namespace lgs {
 // Process-wide kernel choices (lgs_set_option; the initial values come from
 // LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
 // launch path reads the environment).
-enum DecodeKernel { kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4, kDecGroup = 5 };
-// Outputs over the 16 KiB class: the one-tag walk (default), the workgroup
-// decoder (lgs_decode_group.hip; outputs up to the 64 KiB class), or, in the
-// probe library, the trip decoder.
+enum DecodeKernel {
+  kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4, kDecGroup = 5, kDecChain = 6
+};
+// Outputs over the 16 KiB class: the one-tag walk (default), or, in the
+// probe library, the trip decoder or the workgroup decoder.
 enum WideKernel { kWideWalk = 0, kWideTrips = 1, kWideGroup = 2 };
 struct Options {
   std::atomic<int> decoder{kDecAuto};   // DecodeKernel
@@ -51,10 +52,16 @@ hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s);
 #endif
 // The ring decoder (lane per block, large batches), for the split launch.
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
-// The workgroup-per-block decoder (lgs_decode_group.hip): one block per
-// workgroup of 1 024 threads, outputs up to kGroupMaxOut bytes.
+// The chain decoder (lgs_decode_chain.hip): a wave per block, the tag walk
+// apart from the byte moves; outputs up to kChainMaxOut bytes.
+constexpr uint32_t kChainMaxOut = 16896;
+hipError_t launch_decode_chain(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
+#ifdef LGS_PROBE_DECODERS
+// Probe library only (lgs_decode_group.hip): the workgroup (pointer-jumping)
+// decoder, outputs up to kGroupMaxOut bytes.
 constexpr uint32_t kGroupMaxOut = 66048;
 hipError_t launch_decode_group(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
+#endif
 // max_in: largest item length in the launch (<= 65536).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s);
 // Sort a mixed-size batch into size classes on the device: class c holds

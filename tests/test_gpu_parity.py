@@ -208,7 +208,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring", "group"], ["quad", "ops"]))
+@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring", "chain"], ["quad", "ops", "group"]))
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -227,7 +227,7 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave", "group")], [("quad", "ops")]))
+@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave", "chain")], [("quad", "ops", "group")]))
 def test_decode_kernels_c2_full_size(gpu, digests, force, kernels):
     import torch
     from lcdb_amd import batch
@@ -379,7 +379,7 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["ring", "group"], ["quad", "ops"]))
+@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops", "group"]))
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
@@ -512,7 +512,7 @@ if PROBE:   # the two-pass decoder exists in the probe library only
 
 
 
-@pytest.mark.parametrize("kernel", _with_probe([None, "ring", "group"], ["quad", "ops"]))
+@pytest.mark.parametrize("kernel", _with_probe([None, "ring", "chain"], ["quad", "ops", "group"]))
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
@@ -711,7 +711,7 @@ def _trip_stress_stream(rng, want: int) -> bytes:
     return _varint(len(out)) + bytes(s), bytes(out)
 
 
-@pytest.mark.parametrize("wide", _with_probe(["walk", "group"], ["trips"]))
+@pytest.mark.parametrize("wide", _with_probe(["walk"], ["trips", "group"]))
 def test_decode_wide_dependent_copies_and_c3(gpu, digests, force, wide):
     # The wide class (outputs over 16 KiB) on C3 (its 64 KiB fillseq and
     # random classes among the others) and on hand-made streams dense in
@@ -753,8 +753,9 @@ def test_decode_wide_dependent_copies_and_c3(gpu, digests, force, wide):
 
 
 def _group_streams(rng, ref):
-    """Streams for the workgroup decoder's windows (4 096 stream bytes,
-    8 192 output bytes each): real 4 / 16 / 64 KiB blocks, dependent-copy
+    """Streams for the chain decoder's 64-tag batches and the workgroup
+    decoder's windows (4 096 stream bytes, 8 192 output bytes each): real
+    4 / 16 / 64 KiB blocks, dependent-copy
     stress streams, long literals crossing windows, outputs that cut windows
     (64-byte copies of dist 1: 21 output bytes per stream byte), every reject
     placed in the first, a middle and the last window, and their corruptions."""
@@ -803,13 +804,16 @@ def _group_streams(rng, ref):
     return streams
 
 
-@pytest.mark.parametrize("cap", [4608, 16896, 66048])
-def test_decode_group_windows_and_rejects(gpu, force, cap):
-    # The workgroup decoder forced on every stream of _group_streams, at each
-    # of its LDS classes, against the reference's bytes and accept/reject bit
-    # (a header beyond the capacity is LGS_ST_NOSPACE, as in every decoder).
+@pytest.mark.parametrize("kernel,cap", [("chain", 4608), ("chain", 16896)] + (
+    [pytest.param("group", c, marks=pytest.mark.probe) for c in (4608, 16896, 66048)] if PROBE
+    else []))
+def test_decode_small_batch_kernels_and_rejects(gpu, force, kernel, cap):
+    # The chain decoder (and, in the probe library, the workgroup decoder)
+    # forced on every stream of _group_streams, at each of its LDS classes,
+    # against the reference's bytes and accept/reject bit (a header beyond
+    # the capacity is LGS_ST_NOSPACE, as in every decoder).
     import random
-    force("decoder", "group")
+    force("decoder", kernel)
     rng = random.Random(cap)
     ref = oracle.best()
     streams = _group_streams(rng, ref)
@@ -828,9 +832,9 @@ def test_decode_group_windows_and_rejects(gpu, force, cap):
     assert oks >= 20
 
 
-def test_decode_group_dropin_and_odd_outputs(gpu):
-    # Single blocks through the drop-in take the workgroup decoder (n = 1);
-    # outputs at every 16-byte phase exercise its head / tail granules.
+def test_decode_dropin_small_batch_path(gpu):
+    # Single blocks through the drop-in take the chain decoder (n = 1; the
+    # 64 KiB class the wide walk), from the slot's mapped pinned memory.
     import random
     rng = random.Random(5)
     ref = oracle.best()
