@@ -307,14 +307,12 @@ int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
 
 /* Process-wide kernel choices (A/B and tests; the defaults pick by batch):
      "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
-                | "chain" (wave-per-block, the tag walk apart from the byte
-                  moves; outputs up to 16 896 bytes; auto takes it for
-                  batches of at most 32 blocks, e.g. every drop-in call)
      "wide":    "walk"  (decoder of outputs over 16 KiB: the one-tag walk)
      "split":   "1" | "0"  (size-class split of mixed batches, see above)
    Initial values: LGS_DECODE_KERNEL, LGS_NO_SPLIT=1, read once at load.
    LGS_EINVAL for an unknown name or value.  (The decoders that lost their
-   A/B -- "decoder" "quad", "ops" and "group", "wide" "trips" and "group" --
+   A/B -- "decoder" "quad", "ops", "group" and "chain", "wide" "trips" and
+   "group" --
    exist only in the test-only probe library; this library
    rejects them.) */
 int lgs_set_option(const char *name, const char *value);

@@ -25,9 +25,9 @@ CORPUS_LIB = os.path.join(PKG, "libcorpus.so")
 # (lgs_decode_probe.hip, -DLGS_PROBE_DECODERS).  Never loaded by lcdb or the
 # product path; tests/test_gpu_probe_decoders.py runs it in a subprocess.
 PROBE_LIB = os.path.join(PKG, "liblcdb_gpu_snappy_probe.so")
-PROBE_SOURCES = ["lgs_decode_probe.hip", "lgs_decode_group.hip"]
+PROBE_SOURCES = ["lgs_decode_probe.hip", "lgs_decode_group.hip", "lgs_decode_chain.hip"]
 
-HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip", "lgs_decode_chain.hip",
+HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip",
                "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp", "lgs_probe.hip"]
 HIP_HEADERS = ["lgs_device.h", "lgs_launch.h", "lgs_decode_common.h"]
 # Only ldb_snappy_* and lgs_* are exported (the library is loaded into lcdb).

@@ -727,8 +727,8 @@ Options& options_init() {
     const char* dk = getenv("LGS_DECODE_KERNEL");
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
-    if (dk && !strcmp(dk, "chain")) v->decoder = kDecChain;
 #ifdef LGS_PROBE_DECODERS
+    if (dk && !strcmp(dk, "chain")) v->decoder = kDecChain;
     if (dk && !strcmp(dk, "group")) v->decoder = kDecGroup;
     const char* wg = getenv("LGS_WIDE_DECODER");
     if (wg && !strcmp(wg, "group")) v->wide = kWideGroup;
@@ -810,15 +810,15 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
-    else if (!strcmp(value, "chain")) o.decoder = kDecChain;
 #ifdef LGS_PROBE_DECODERS
+    else if (!strcmp(value, "chain")) o.decoder = kDecChain;
     else if (!strcmp(value, "group")) o.decoder = kDecGroup;
     // The decoders that lost their A/B exist in the probe library only
     // (lgs_decode_probe.hip); the product rejects them.
     else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
     else if (!strcmp(value, "ops")) o.decoder = kDecOps;
 #endif
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring, wave or chain)", value);
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)

@@ -972,9 +972,6 @@ constexpr uint32_t kDecCap2 = 66048;   // 64 KiB class (+ block-builder overshoo
 // batch).  On incompressible blocks the wave kernel wins at every size
 // (98 against 163 us at 49 152), but a launch does not know the ratio.
 constexpr uint32_t kLaneMinBlocks = 36864;
-// Batches of at most this many blocks go to the chain decoder (the tag walk
-// apart from the byte moves: latency-bound single blocks).
-constexpr uint32_t kChainMaxBlocks = 32;
 
 // ---------------------------------------------------------------------------
 // Mixed-size batches.  One launch sized for its largest block runs every
@@ -1126,12 +1123,8 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
     return launch_decode_ring(a, s);
 #ifdef LGS_PROBE_DECODERS
   if (force == kDecGroup && max_out <= kGroupMaxOut) return launch_decode_group(a, max_out, s);
+  if (force == kDecChain && max_out <= kChainMaxOut) return launch_decode_chain(a, max_out, s);
 #endif
-  // A few blocks: each one's serial tag chain is the launch's latency, so
-  // the chain decoder walks it apart from the byte moves.
-  if ((force == kDecChain || (force == kDecAuto && a.n <= kChainMaxBlocks)) &&
-      max_out <= kChainMaxOut)
-    return launch_decode_chain(a, max_out, s);
   if (max_out <= kDecCap0) return launch_decode_cls<kDecCap0, 1>(a, s);
   if (max_out <= kDecCap1) return launch_decode_mid(a, s);
   return launch_decode_big(a, max_out, s);

@@ -1,6 +1,10 @@
 // lgs_decode_chain.hip -- wave-per-block Snappy decoder for the batches where
 // latency, not throughput, is the bound: the drop-in's single blocks and
-// other batches of a few blocks (fewer blocks than the chip has SIMDs).
+// other batches of a few blocks.  PROBE LIBRARY ONLY (-DLGS_PROBE_DECODERS):
+// exact, but it loses -- 36 us for one 4 KiB block against the wave
+// decoder's 28 (profiles/r4i_session.txt): a lone wave pays ~4 cycles an
+// instruction whatever they depend on, and walking the chain then moving
+// the bytes issues about as many instructions as doing both per tag.
 //
 // Semantics: lcdb src/util/snappy.c:386-412 and decode_blocks (:201-341),
 // with every reject of :216-338 and :337.  The other decoders move each
@@ -23,6 +27,9 @@
 // each other; a copy reads only bytes before its own output, all written by
 // then.  A stream longer than the LDS staging area (never a valid 4 KiB
 // block from lcdb) is decoded by decode_stream from global memory.
+#ifndef LGS_PROBE_DECODERS
+#error "lgs_decode_chain.hip is built into the probe library only (build.py build_probe)"
+#endif
 #include "lgs_device.h"
 #include "lgs_decode_common.h"
 #include "lgs_launch.h"

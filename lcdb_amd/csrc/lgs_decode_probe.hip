@@ -741,7 +741,16 @@ __global__ __launch_bounds__(64) void decode_quad_kernel(
       const uint32_t pc = longl ? 64u : len;
       const uint32_t lp = my_p + hl;                           // a literal's first byte
       const uint32_t cs = my_m - dist;                         // a copy's first source byte
+#ifdef LGS_PROBE_QUAD_OLD_NEAR
+      // Round 3's rule: the near window grew with the slot's
+      // offset in the trip, which admits 256 < dist <= 368 as ring reads --
+      // a slot an earlier op of the same trip has already overwritten.
       const bool far = !lit & (dist > kNear + (my_m - made0));
+#else
+      // Near = in the 256-byte ring and not overwritten by this trip: a
+      // constant bound below the ring size, as in the ring decoder.
+      const bool far = !lit & (dist > kNear);
+#endif
       const bool ok = hdr & !bad & (!lit | (lp + pc <= in_have)) & (!far | (cs + len <= F0)) &
                       ((g == 0) | (my_m + pc - made0 <= kBudget)) & !(longl & (g > 0));
       // the longest prefix of passing slots, none after a far copy or a long

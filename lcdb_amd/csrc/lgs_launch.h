@@ -52,15 +52,15 @@ hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s);
 #endif
 // The ring decoder (lane per block, large batches), for the split launch.
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
-// The chain decoder (lgs_decode_chain.hip): a wave per block, the tag walk
-// apart from the byte moves; outputs up to kChainMaxOut bytes.
-constexpr uint32_t kChainMaxOut = 16896;
-hipError_t launch_decode_chain(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
 #ifdef LGS_PROBE_DECODERS
-// Probe library only (lgs_decode_group.hip): the workgroup (pointer-jumping)
-// decoder, outputs up to kGroupMaxOut bytes.
+// Probe library only: the workgroup (pointer-jumping) decoder of
+// lgs_decode_group.hip, outputs up to kGroupMaxOut bytes, and the chain
+// decoder of lgs_decode_chain.hip (a wave per block, the tag walk apart
+// from the byte moves), outputs up to kChainMaxOut bytes.
 constexpr uint32_t kGroupMaxOut = 66048;
 hipError_t launch_decode_group(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
+constexpr uint32_t kChainMaxOut = 16896;
+hipError_t launch_decode_chain(const DecodeArgs& a, uint32_t max_out, hipStream_t s);
 #endif
 // max_in: largest item length in the launch (<= 65536).
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s);

@@ -124,18 +124,17 @@ def test_product_has_only_the_kept_decoders():
     their kernels nor accepts their options (lgs_set_option needs no GPU)."""
     blob = open(build.LIB, "rb").read()
     for k in (b"decode_quad_kernel", b"tag_scan_kernel", b"op_exec_kernel",
-              b"decode_trips_kernel", b"decode_group_kernel"):
+              b"decode_trips_kernel", b"decode_group_kernel", b"decode_chain_kernel"):
         assert k not in blob, k
-    for k in (b"decode_ring_kernel", b"decode_wide_kernel", b"decode_kernel",
-              b"decode_chain_kernel"):
+    for k in (b"decode_ring_kernel", b"decode_wide_kernel", b"decode_kernel"):
         assert k in blob, k
     lib = _native.lib()
     for name, value in (("decoder", "quad"), ("decoder", "ops"), ("decoder", "group"),
-                        ("wide", "trips"), ("wide", "group")):
+                        ("decoder", "chain"), ("wide", "trips"), ("wide", "group")):
         assert lib.lgs_set_option(name.encode(), value.encode()) == _native.LGS_EINVAL, value
-    for name, value in (("decoder", "ring"), ("decoder", "wave"), ("decoder", "chain"),
-                        ("decoder", "auto"), ("wide", "walk")):
+    for name, value in (("decoder", "ring"), ("decoder", "wave"), ("decoder", "auto"),
+                        ("wide", "walk")):
         assert lib.lgs_set_option(name.encode(), value.encode()) == _native.LGS_OK, value
     probe = open(build.PROBE_LIB, "rb").read()
     assert b"decode_quad_kernel" in probe and b"op_exec_kernel" in probe
-    assert b"decode_group_kernel" in probe
+    assert b"decode_group_kernel" in probe and b"decode_chain_kernel" in probe

@@ -208,7 +208,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring", "chain"], ["quad", "ops", "group"]))
+@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops", "group", "chain"]))
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -227,7 +227,7 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave", "chain")], [("quad", "ops", "group")]))
+@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops", "group", "chain")]))
 def test_decode_kernels_c2_full_size(gpu, digests, force, kernels):
     import torch
     from lcdb_amd import batch
@@ -512,7 +512,7 @@ if PROBE:   # the two-pass decoder exists in the probe library only
 
 
 
-@pytest.mark.parametrize("kernel", _with_probe([None, "ring", "chain"], ["quad", "ops", "group"]))
+@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops", "group", "chain"]))
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
@@ -804,12 +804,13 @@ def _group_streams(rng, ref):
     return streams
 
 
-@pytest.mark.parametrize("kernel,cap", [("chain", 4608), ("chain", 16896)] + (
-    [pytest.param("group", c, marks=pytest.mark.probe) for c in (4608, 16896, 66048)] if PROBE
+@pytest.mark.parametrize("kernel,cap", [("wave", 4608), ("wave", 16896), ("wave", 66048)] + (
+    [pytest.param("group", c, marks=pytest.mark.probe) for c in (4608, 16896, 66048)] +
+    [pytest.param("chain", c, marks=pytest.mark.probe) for c in (4608, 16896)] if PROBE
     else []))
 def test_decode_small_batch_kernels_and_rejects(gpu, force, kernel, cap):
-    # The chain decoder (and, in the probe library, the workgroup decoder)
-    # forced on every stream of _group_streams, at each of its LDS classes,
+    # The wave decoder (and, in the probe library, the workgroup and chain
+    # decoders) forced on every stream of _group_streams, at each LDS class,
     # against the reference's bytes and accept/reject bit (a header beyond
     # the capacity is LGS_ST_NOSPACE, as in every decoder).
     import random
@@ -833,8 +834,8 @@ def test_decode_small_batch_kernels_and_rejects(gpu, force, kernel, cap):
 
 
 def test_decode_dropin_small_batch_path(gpu):
-    # Single blocks through the drop-in take the chain decoder (n = 1; the
-    # 64 KiB class the wide walk), from the slot's mapped pinned memory.
+    # Single blocks through the drop-in (the wave decoder; the 64 KiB class
+    # the wide walk), from the slot's mapped pinned memory.
     import random
     rng = random.Random(5)
     ref = oracle.best()

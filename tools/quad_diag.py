@@ -115,6 +115,19 @@ def main() -> None:
                 first = {"byte": int(w), "op": j, "kind": kind, "at": at, "len": ln, "dist": d,
                          "stream_pos": sp, "got": v, "want": int(ref[w])}
         tot["wrong_bytes"] += len(wrong)
+        if len(lines) < maxb and first is not None:
+            # what the first wrong op's bytes equal: output at another
+            # distance, or stream bytes somewhere
+            at, ln = first["at"], first["len"]
+            gotb = bytes(got[at:at + ln])
+            first["got_bytes"] = gotb.hex()
+            first["want_bytes"] = bytes(ref[at:at + ln]).hex()
+            first["as_output_dist"] = [d for d in range(1, at + 1)
+                                       if bytes(ref[at - d:at - d + ln]) == gotb][:8]
+            first["as_stream_pos"] = [x for x in range(len(stream) - ln)
+                                      if stream[x:x + ln] == gotb][:8]
+            first["as_got_output_dist"] = [d for d in range(1, at + 1)
+                                           if bytes(got[at - d:at - d + ln]) == gotb][:8]
         if len(lines) < maxb:
             lines.append({"block": i, "status": int(sts[i]), "wrong": int(len(wrong)),
                           "by_op_class": dict(per), "first": first,
