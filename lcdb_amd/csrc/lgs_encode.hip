@@ -754,6 +754,12 @@ __global__ __launch_bounds__(64) void encode_kernel(
   const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
   const OutSlot o = out_slot(out, uni64(out_off[i]), len);
 
+#ifdef LGS_PROBE_ENC_TIMING
+  // probe (tools/enc_phases.py): shader-clock stamps of this wave's phases,
+  // stored in the last 16 bytes of its output slot (past the encoding)
+  const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+  uint64_t tp1 = tp0;
+#endif
   uint32_t op = emit_header(o, uni(hdr ? hdr[i] : len));
 
   // snappy.c:370-381: independent 64 KiB chunks, a short tail as a literal.
@@ -767,6 +773,10 @@ __global__ __launch_bounds__(64) void encode_kernel(
     stage_in_linear<kR>(s.img, src + c0, clen);
     LdsIn x{s.img};
     order();
+#ifdef LGS_PROBE_ENC_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    tp1 = __builtin_amdgcn_s_memtime();
+#endif
     if (clen >= kMinBlock) {
       op = encode_chunk<kImg>(x, clen, s.tab, o, op, pl);
     } else {
@@ -774,6 +784,16 @@ __global__ __launch_bounds__(64) void encode_kernel(
     }
     order();
   }
+#ifdef LGS_PROBE_ENC_TIMING
+  __builtin_amdgcn_s_waitcnt(0);
+  const uint64_t tp2 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {
+    const uint32_t b = 32 + len + len / 6 - 16;
+    o.put4(0, b, (uint32_t)(tp1 - tp0));
+    o.put4(0, b + 4, (uint32_t)(tp2 - tp1));
+    o.put4(0, b + 8, 0x7e57u);
+  }
+#endif
   if (lane == 0) out_len[i] = op;
 }
 
