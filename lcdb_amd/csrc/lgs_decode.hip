@@ -739,9 +739,11 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           const uint8_t* sp = lit ? ib + (olp & (kInRing - 1))
                                   : ob + ((made - dist) & (kOutRing - 1));
           const u32x4 c0 = lrd16(sp);
-          // Period 1/2/4/8: the dist bytes before d as a 16-byte pattern.
-          const uint32_t b0 = c0.x & 0xffu, h0 = c0.x & 0xffffu;
-          const uint32_t w1 = b0 * 0x01010101u, w2 = h0 | (h0 << 16);
+          // Period 1/2/4/8: the dist bytes before d as a 16-byte pattern
+          // (byte 0 four times, bytes 0-1 twice: one v_perm each, not a
+          // quarter-rate v_mul_lo_u32).
+          const uint32_t w1 = __builtin_amdgcn_perm(c0.x, c0.x, 0x00000000u);
+          const uint32_t w2 = __builtin_amdgcn_perm(c0.x, c0.x, 0x01000100u);
           const uint32_t px = dist == 1 ? w1 : (dist == 2 ? w2 : c0.x);
           const uint32_t py = dist == 8 ? c0.y : px;
           const u32x4 pv = {px, py, px, py};
@@ -786,7 +788,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       // Flushed already: it ends <= made - kNear + 64 < F.  All 64 bytes are
       // loaded whatever the length (one exec-mask region, not four nested):
       // dist > kNear puts even the 64th inside [0, F) of this block.
-      const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + made - odist);
+      const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + (made - odist));   // 32-bit offset
 #ifndef LGS_PROBE_NOFAR
       fa0 = ld16(sp);
       fa1 = ld16(sp + 16);

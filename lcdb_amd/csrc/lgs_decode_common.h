@@ -219,8 +219,10 @@ __device__ __forceinline__ Tag parse_tag(u32x4 tv, uint32_t pos, uint32_t slen, 
   // also needs m < 2^31 - 1 (:258) and its bytes in the stream (:263); a
   // copy needs 0 < dist <= made (:320, :323): dist - 1 >= made as unsigned
   // covers dist == 0 and dist >= 2^31 too, since made < 2^31.
+  // (As lane masks, not a select of two bools: a select of bools goes
+  // through a VGPR and back.)
   t.bad = (t.hl > left) | (t.len > want - made) |
-          (lit ? (m >= 0x7fffffffu) | (t.hl + t.len > left) : (cdist - 1 >= made));
+          (lit & ((m >= 0x7fffffffu) | (t.hl + t.len > left))) | (!lit & (cdist - 1 >= made));
   t.next = pos + t.hl + (lit ? t.len : 0u);
   return t;
 }
