@@ -499,8 +499,9 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
 // PCIe, no hipMemcpy) and synchronises once.
 
 // How a drop-in call waits for its one launch: by polling an event recorded
-// after it (the calling thread spins for the kernel's few tens of us), or in
-// hipStreamSynchronize.  LGS_DROPIN_WAIT=block / poll, read once.
+// after it for up to 200 us (a block's kernel takes ~30), then blocking in
+// hipEventSynchronize; or, LGS_DROPIN_WAIT=block (read once), in
+// hipStreamSynchronize from the start.
 bool dropin_poll() {
   static const bool poll = [] {
     const char* v = getenv("LGS_DROPIN_WAIT");
@@ -516,8 +517,13 @@ int slot_wait(Ctx& c) {
   }
   if (!c.polled) LGS_HIP(hipEventCreateWithFlags(&c.polled, hipEventDisableTiming));
   LGS_HIP(hipEventRecord(c.polled, c.stream));
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e;
   while ((e = hipEventQuery(c.polled)) == hipErrorNotReady) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+      LGS_HIP(hipEventSynchronize(c.polled));
+      return LGS_OK;
+    }
   }
   LGS_HIP(e);
   return LGS_OK;
