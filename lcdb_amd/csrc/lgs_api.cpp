@@ -167,7 +167,6 @@ struct Ctx {
   size_t h_cap = 0;
   uint8_t* h_dev = nullptr; // a drop-in slot's pinned arena as the device sees it
   bool fixed = false;       // a drop-in slot: arenas never grow
-  hipEvent_t polled = nullptr;   // a drop-in call's completion, polled (slot_wait)
 };
 
 // lgs_set_device() choice of the calling thread (-1: its current device).
@@ -498,37 +497,6 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
 // into it, launches the kernel on it (input read and output written over
 // PCIe, no hipMemcpy) and synchronises once.
 
-// How a drop-in call waits for its one launch: by polling an event recorded
-// after it for up to 200 us (a block's kernel takes ~30), then blocking in
-// hipEventSynchronize; or, LGS_DROPIN_WAIT=block (read once), in
-// hipStreamSynchronize from the start.
-bool dropin_poll() {
-  static const bool poll = [] {
-    const char* v = getenv("LGS_DROPIN_WAIT");
-    return !(v && !strcmp(v, "block"));
-  }();
-  return poll;
-}
-
-int slot_wait(Ctx& c) {
-  if (!dropin_poll()) {
-    LGS_HIP(hipStreamSynchronize(c.stream));
-    return LGS_OK;
-  }
-  if (!c.polled) LGS_HIP(hipEventCreateWithFlags(&c.polled, hipEventDisableTiming));
-  LGS_HIP(hipEventRecord(c.polled, c.stream));
-  const auto t0 = std::chrono::steady_clock::now();
-  hipError_t e;
-  while ((e = hipEventQuery(c.polled)) == hipErrorNotReady) {
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
-      LGS_HIP(hipEventSynchronize(c.polled));
-      return LGS_OK;
-    }
-  }
-  LGS_HIP(e);
-  return LGS_OK;
-}
-
 // Device bytes one 64 KiB-or-less chunk takes in a pass.
 constexpr size_t kChunkIn = kChunk + 16;                         // its input
 size_t chunk_out(uint32_t len) { return align_up(bound_of(len) + 8, 16); }
@@ -592,7 +560,7 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
                  (const uint64_t*)(hd + o_ooff), (uint32_t*)(hd + o_olen),
                  (const uint32_t*)(hd + o_hdr), nullptr, k, nullptr};
     LGS_HIP(launch_encode(a, k == 1 ? ilen[0] : kChunk, c.stream));
-    LGS_TRY(slot_wait(c));
+    LGS_HIP(hipStreamSynchronize(c.stream));
     const uint32_t* olen = (const uint32_t*)(h + o_olen);
     for (uint32_t j = 0; j < k; ++j) {
       if (olen[j] > chunk_out(ilen[j]))
@@ -706,7 +674,7 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
                  (const uint64_t*)(hd + o_ooff), (const uint32_t*)(hd + o_ocap),
                  (uint32_t*)(hd + o_olen), hd + o_st, nullptr, 1, nullptr};
     LGS_HIP(launch_decode(a, want, c.stream));
-    LGS_TRY(slot_wait(c));
+    LGS_HIP(hipStreamSynchronize(c.stream));
     const uint8_t st = h[o_st];
     if (st == LGS_ST_OK) memcpy(zp, h + o_out, want);
     *ok = st == LGS_ST_OK;

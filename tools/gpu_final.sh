@@ -11,8 +11,7 @@ timeout -k 10 900 $T tests -m gpu > gpurun_out/r4z_pytest_gpu.txt 2>&1 || { tail
 tail -3 gpurun_out/r4z_pytest_gpu.txt
 NO_TDB=1 REPS=1000 timeout -k 10 300 python tools/bench_dropin_latency.py > gpurun_out/r4z_dropin.json 2>&1 || exit 1
 REPS=300 timeout -k 10 200 python tools/dropin_breakdown.py > gpurun_out/r4z_breakdown.json 2>&1 || exit 1
-LGS_DROPIN_WAIT=block NO_TDB=1 REPS=1000 timeout -k 10 300 python tools/bench_dropin_latency.py > gpurun_out/r4z_dropin_block.json 2>&1 || exit 1
-grep -v amdgpu.ids gpurun_out/r4z_dropin.json | head -c 300; echo; grep -v amdgpu.ids gpurun_out/r4z_dropin_block.json | head -c 300; echo
+grep -v amdgpu.ids gpurun_out/r4z_dropin.json | head -c 300; echo
 timeout -k 10 600 python bench.py > gpurun_out/r4z_bench.json 2> gpurun_out/r4z_bench.err || { tail -5 gpurun_out/r4z_bench.err; exit 1; }
 grep '^{' gpurun_out/r4z_bench.json | tail -1 | head -c 1500; echo
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r4z_bench -o bench --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-pipelined --no-cpu-baseline --no-c3 > gpurun_out/r4z_bench_under_rocprof.json 2> gpurun_out/r4z_bench_under_rocprof.err || { tail -5 gpurun_out/r4z_bench_under_rocprof.err; exit 1; }
