@@ -3,6 +3,8 @@
 
   kernel    the batch kernel on that one block, device-resident, HIP events
             (the block's serial chain on one wave of an idle GPU)
+  floor     the same 16-byte copy kernel between two HIP events (what the
+            event pair adds to a kernel time above)
   launch    an empty-work launch + stream synchronisation through the same
             library (lgs_hbm_copy_dev of 16 bytes, then torch.cuda.synchronize)
   dropin    ldb_snappy_encode / ldb_snappy_decode from the host (pageable
@@ -67,6 +69,8 @@ def main() -> None:
         L.lgs_hbm_copy_dev(C.c_void_p(b.data_ptr()), C.c_void_p(a.data_ptr()), 16, None)
         torch.cuda.synchronize()
     res["launch_sync_us"] = wall(empty)
+    res["event_floor_us"] = ev_time(lambda: L.lgs_hbm_copy_dev(
+        C.c_void_p(b.data_ptr()), C.c_void_p(a.data_ptr()), 16, C.c_void_p(s.cuda_stream)))
     blk = bytes(c.buf[c.off[0]:c.off[0] + c.len[0]])
     src = C.create_string_buffer(blk + b"\0" * 16, len(blk) + 16)
     dst = C.create_string_buffer(8192)
