@@ -559,6 +559,7 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
     EncodeArgs a{hd, (const uint64_t*)(hd + o_ioff), (const uint32_t*)(hd + o_ilen), hd,
                  (const uint64_t*)(hd + o_ooff), (uint32_t*)(hd + o_olen),
                  (const uint32_t*)(hd + o_hdr), nullptr, k, nullptr};
+    if (k == 1) a.one = Item1{ioff[0], ooff[0], ilen[0], hdr[0], 1};
     LGS_HIP(launch_encode(a, k == 1 ? ilen[0] : kChunk, c.stream));
     LGS_HIP(hipStreamSynchronize(c.stream));
     const uint32_t* olen = (const uint32_t*)(h + o_olen);
@@ -673,6 +674,7 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
     DecodeArgs a{hd, (const uint64_t*)(hd + o_ioff), (const uint32_t*)(hd + o_ilen), hd,
                  (const uint64_t*)(hd + o_ooff), (const uint32_t*)(hd + o_ocap),
                  (uint32_t*)(hd + o_olen), hd + o_st, nullptr, 1, nullptr};
+    a.one = Item1{o_in, o_out, n, want, 1};
     LGS_HIP(launch_decode(a, want, c.stream));
     LGS_HIP(hipStreamSynchronize(c.stream));
     const uint8_t st = h[o_st];

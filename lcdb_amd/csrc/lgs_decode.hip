@@ -215,7 +215,7 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
     const uint32_t* __restrict__ index, uint32_t n,
-    const uint32_t* __restrict__ count) {
+    const uint32_t* __restrict__ count, const Item1 one) {
   // One in-place buffer per wave: the output image grows from the bottom,
   // the compressed stream is staged at the top (+ 48 for its alignment
   // shift and zero pad, + 256 so the window reads of decode_win never read
@@ -233,10 +233,16 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
 
-  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
-  const uint32_t slen = uni(in_len[i]);
-  const gptr<uint8_t> dst = to_global(out) + uni64(out_off[i]);
-  const uint32_t cap = uni(out_cap[i] < OUT_CAP ? out_cap[i] : OUT_CAP);
+  uint64_t ioff, ooff;
+  uint32_t slen, cap;
+  if (one.on) {                                     // the drop-in's item, by value
+    ioff = one.in_off; ooff = one.out_off; slen = one.in_len; cap = one.aux;
+  } else {
+    ioff = uni64(in_off[i]); ooff = uni64(out_off[i]); slen = uni(in_len[i]); cap = uni(out_cap[i]);
+  }
+  cap = cap < OUT_CAP ? cap : OUT_CAP;
+  const gptr<const uint8_t> src = to_global(in) + ioff;
+  const gptr<uint8_t> dst = to_global(out) + ooff;
   const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
   uint8_t* o = &s_buf[wv][oshift];
 
@@ -558,7 +564,7 @@ static hipError_t launch_decode_cls(const DecodeArgs& a, hipStream_t s) {
   const uint32_t grid = (a.n + WAVES - 1) / WAVES;
   hipLaunchKernelGGL((decode_kernel<OUT_CAP, WAVES>), dim3(grid), dim3(64 * WAVES), 0, s,
                      a.in, a.in_off, a.in_len, a.out, a.out_off, a.out_cap, a.out_len, a.status,
-                     a.index, a.n, a.count);
+                     a.index, a.n, a.count, a.one);
   return hipGetLastError();
 }
 

@@ -736,7 +736,7 @@ __global__ __launch_bounds__(64) void encode_kernel(
     const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
     const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
     const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
-    const uint32_t* __restrict__ count) {
+    const uint32_t* __restrict__ count, const Item1 one) {
   // Image: + 48 the zero granule past it (and spare), + 64 the match
   // extension's reads past the chunk (encode_chunk).  8 832 B with the
   // table: 18 waves per CU (the 1 280-byte LDS granule).
@@ -750,9 +750,16 @@ __global__ __launch_bounds__(64) void encode_kernel(
   const uint32_t lane = lane_id();
   const PostLanes pl = post_lanes(lane);
 
-  const uint32_t len = uni(in_len[i]);
-  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
-  const OutSlot o = out_slot(out, uni64(out_off[i]), len);
+  uint64_t ioff, ooff;
+  uint32_t len, hv;
+  if (one.on) {                                     // the drop-in's item, by value
+    ioff = one.in_off; ooff = one.out_off; len = one.in_len; hv = one.aux;
+  } else {
+    ioff = uni64(in_off[i]); ooff = uni64(out_off[i]); len = uni(in_len[i]);
+    hv = uni(hdr ? hdr[i] : len);
+  }
+  const gptr<const uint8_t> src = to_global(in) + ioff;
+  const OutSlot o = out_slot(out, ooff, len);
 
 #ifdef LGS_PROBE_ENC_TIMING
   // probe (tools/enc_phases.py): shader-clock stamps of this wave's phases,
@@ -760,7 +767,7 @@ __global__ __launch_bounds__(64) void encode_kernel(
   const uint64_t tp0 = __builtin_amdgcn_s_memtime();
   uint64_t tp1 = tp0;
 #endif
-  uint32_t op = emit_header(o, uni(hdr ? hdr[i] : len));
+  uint32_t op = emit_header(o, hv);
 
   // snappy.c:370-381: independent 64 KiB chunks, a short tail as a literal.
   // (IN_CAP >= min(len, 65536) is guaranteed by the launcher.)
@@ -843,7 +850,7 @@ template <uint32_t IN_CAP>
 static hipError_t launch_encode_cls(const EncodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((encode_kernel<IN_CAP>), dim3(a.n), dim3(64), 0, s, a.in,
                      a.in_off, a.in_len, a.out, a.out_off, a.out_len, a.hdr, a.index, a.n,
-                     a.count);
+                     a.count, a.one);
   return hipGetLastError();
 }
 

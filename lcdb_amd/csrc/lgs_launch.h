@@ -27,11 +27,23 @@ struct Options {
 };
 Options& options();
 
+// One work item's offsets and lengths passed by value (the drop-in, whose
+// per-item arrays sit in mapped host memory: reading them would cost the
+// kernel a PCIe round trip before it can load the stream).  on == 0: the
+// kernels read the arrays.  Kernels that do not take it read the arrays,
+// which the drop-in fills as well.
+struct Item1 {
+  uint64_t in_off = 0, out_off = 0;
+  uint32_t in_len = 0, aux = 0;   // aux: decode out_cap, encode hdr
+  uint32_t on = 0;
+};
+
 struct DecodeArgs {
   const uint8_t* in; const uint64_t* in_off; const uint32_t* in_len;
   uint8_t* out; const uint64_t* out_off; const uint32_t* out_cap;
   uint32_t* out_len; uint8_t* status; const uint32_t* index; uint32_t n;
   const uint32_t* count;   // device count of index[] entries (nullptr: n)
+  Item1 one{};             // item 0 by value (decode_kernel)
 };
 
 struct EncodeArgs {
@@ -39,6 +51,7 @@ struct EncodeArgs {
   uint8_t* out; const uint64_t* out_off; uint32_t* out_len;
   const uint32_t* hdr; const uint32_t* index; uint32_t n;
   const uint32_t* count;   // device count of index[] entries (nullptr: n)
+  Item1 one{};             // item 0 by value (encode_kernel)
 };
 
 // max_out: largest out_cap in the launch (selects the LDS class).
