@@ -233,6 +233,13 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
 
+#ifdef LGS_PROBE_DEC_TIMING
+  // probe (tools/dec_phases.py): shader-clock stamps of this wave's phases
+  // and the 100 MHz real-time clock, stored in the last 16 bytes of its
+  // output capacity (the tool gives every block 32 bytes of spare capacity)
+  const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   uint64_t ioff, ooff;
   uint32_t slen, cap;
   if (one.on) {                                     // the drop-in's item, by value
@@ -252,8 +259,27 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     constexpr uint32_t kR = (kBuf + 1023) / 1024 < 8 ? (kBuf + 1023) / 1024 : 8;
     const uint32_t sh = stage_in<kR>(&s_buf[wv][ib], src, slen);
     order();
+#ifdef LGS_PROBE_DEC_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t tp1 = __builtin_amdgcn_s_memtime();
+#endif
     st = decode_win(&s_buf[wv][ib], sh, slen, o, (int32_t)ib - (int32_t)oshift, cap, &want);
     order();
+#ifdef LGS_PROBE_DEC_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t tp2 = __builtin_amdgcn_s_memtime();
+    flush_out(dst, &s_buf[wv][0], want);
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t tp3 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt3 = __builtin_amdgcn_s_memrealtime();
+    if (lane_id() == 0) {
+      gptr<uint32_t> q = (gptr<uint32_t>)(dst + ((out_cap[i] - 16) & ~3u));
+      q[0] = (uint32_t)(tp1 - tp0);
+      q[1] = (uint32_t)(tp2 - tp1);
+      q[2] = (uint32_t)(tp3 - tp2);
+      q[3] = (uint32_t)(rt3 - rt0);
+    }
+#endif
   }
   if (st == 3) st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
   if (st == 1) flush_out(dst, &s_buf[wv][0], want);
