@@ -21,6 +21,7 @@
 #include "lgs_device.h"
 #include "lgs_decode_common.h"
 #include "lgs_launch.h"
+#include "lgs_probe_hooks.h"
 
 #include <mutex>
 
@@ -233,13 +234,7 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
 
-#ifdef LGS_PROBE_DEC_TIMING
-  // probe (tools/dec_phases.py): shader-clock stamps of this wave's phases
-  // and the 100 MHz real-time clock, stored in the last 16 bytes of its
-  // output capacity (the tool gives every block 32 bytes of spare capacity)
-  const uint64_t tp0 = __builtin_amdgcn_s_memtime();
-  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
+  LGS_DEC_PH_DECL;
   uint64_t ioff, ooff;
   uint32_t slen, cap;
   if (one.on) {                                     // the drop-in's item, by value
@@ -259,27 +254,11 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     constexpr uint32_t kR = (kBuf + 1023) / 1024 < 8 ? (kBuf + 1023) / 1024 : 8;
     const uint32_t sh = stage_in<kR>(&s_buf[wv][ib], src, slen);
     order();
-#ifdef LGS_PROBE_DEC_TIMING
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t tp1 = __builtin_amdgcn_s_memtime();
-#endif
+    LGS_DEC_PH_STAGED();
     st = decode_win(&s_buf[wv][ib], sh, slen, o, (int32_t)ib - (int32_t)oshift, cap, &want);
     order();
-#ifdef LGS_PROBE_DEC_TIMING
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t tp2 = __builtin_amdgcn_s_memtime();
-    flush_out(dst, &s_buf[wv][0], want);
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint64_t tp3 = __builtin_amdgcn_s_memtime();
-    const uint64_t rt3 = __builtin_amdgcn_s_memrealtime();
-    if (lane_id() == 0) {
-      gptr<uint32_t> q = (gptr<uint32_t>)(dst + ((out_cap[i] - 16) & ~3u));
-      q[0] = (uint32_t)(tp1 - tp0);
-      q[1] = (uint32_t)(tp2 - tp1);
-      q[2] = (uint32_t)(tp3 - tp2);
-      q[3] = (uint32_t)(rt3 - rt0);
-    }
-#endif
+    LGS_DEC_PH_END(flush_out(dst, &s_buf[wv][0], want),
+                   (gptr<uint32_t>)(dst + ((out_cap[i] - 16) & ~3u)));
   }
   if (st == 3) st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
   if (st == 1) flush_out(dst, &s_buf[wv][0], want);
@@ -633,6 +612,21 @@ constexpr uint32_t kInSink = kInRing + 64;             // a lane's sink slot (it
 }  // namespace ring
 
 
+// The tag's 5 bytes (parse_tag reads tv.x and the low byte of tv.y) from
+// two aligned dwords: an unaligned ds_read_b128 is replayed (+~60 LDS
+// cycles; the ring's SQ_LDS_UNALIGNED_STALL was 55 % of its LDS-busy
+// cycles on C2, profiles/r5c_pmc.txt).  (The pieces' 16-byte accesses stay
+// ds_read/write_b128: as aligned dwords (5 reads + v_alignbyte, a write as
+// 3 bytes + 4 dwords) they are exact and slower, 339 against 274 us, and
+// even wrong-byte aligned b128s gain only 3 % -- the instructions, not the
+// LDS cycles, are what a trip waits on; profiles/r5d_ab.txt.)
+__device__ __forceinline__ u32x4 rrd_tag(const uint8_t* p) {
+  const uint32_t r = (uint32_t)(uintptr_t)p & 3u;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p - r);
+  const uint32_t d0 = w[0], d1 = w[1];
+  return u32x4{__builtin_amdgcn_alignbyte(d1, d0, r), d1 >> (8 * r), 0u, 0u};
+}
+
 // 16 bytes at output offset p of a lane's ring (ob = ring start): the ring
 // copy, plus the mirror copy (r < 64) or the wrapped part (r > 240), which
 // only those lanes write.
@@ -784,6 +778,10 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
           // a pattern).  A source chunk can share ring slots only with a
           // later destination chunk (dist <= 240), so reading chunk k just
           // before writing chunk k keeps every read ahead of its clobber.
+          // (All four reads issued before the first write -- legal here, no
+          // source chunk holds a byte the piece writes -- is slower: 292-294
+          // against 273-275 us on C2, profiles/r5b_ab.txt.  The LDS pipe, not
+          // the round trips, is what a piece waits on.)
           if (piece > 16) out_put(ob, made + 16, pat ? pv : lrd16(sp + 16));
           if (piece > 32) out_put(ob, made + 32, pat ? pv : lrd16(sp + 32));
           if (piece > 48) out_put(ob, made + 48, pat ? pv : lrd16(sp + 48));
@@ -804,7 +802,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     // are not parsing read their own ring (in range) and discard the tag.
     const uint32_t need_to = slen - pos < 5 ? slen : pos + 5;
     const bool ready = (st == 1) & (orem == 0) & (pos < slen) & (in_have >= need_to);
-    const Tag t = parse_tag(lrd16(ib + (pos & (kInRing - 1))), pos, slen, want, made);
+    const Tag t = parse_tag(rrd_tag(ib + (pos & (kInRing - 1))), pos, slen, want, made);
     const bool far = (t.kind != 0) & (t.dist > kNear);
     if (ready & t.bad) st = 0;
     // (A far copy parsed in the second slot must find its source flushed
@@ -817,41 +815,47 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     pos = take ? t.next : pos;
     ofar = take ? far : ofar;
     if (take & far) {
-      // Flushed already: it ends <= made - kNear + 64 < F.  All 64 bytes are
-      // loaded whatever the length (one exec-mask region, not four nested):
-      // dist > kNear puts even the 64th inside [0, F) of this block.
+      // The copy's own bytes are flushed already (first slot: they end <=
+      // made - kNear + 64 < F; second slot: the take test above).  A granule
+      // reads up to 15 bytes past the copy; they lie inside [0, made) of this
+      // block (dist > kNear), may be bytes not yet flushed, and are never
+      // used (the landing writes only orem bytes' worth that count).
       const gptr<const uint8_t> sp = (gptr<const uint8_t>)(dst + (made - odist));   // 32-bit offset
-#ifndef LGS_PROBE_NOFAR
-      fa0 = ld16(sp);
-      fa1 = ld16(sp + 16);
-      fa2 = ld16(sp + 32);
-      fa3 = ld16(sp + 48);
-#else
-      (void)sp;
-      fa0 = fa1 = fa2 = fa3 = u32x4{0, 0, 0, 0};
-#endif
+      fa0 = LGS_RING_FAR_LD16(sp);
+      // Only the 16-byte granules the copy has: most far copies are 4-6
+      // bytes (a key's shared prefix), and loading all 64 fetched 232 MB for
+      // 70 MB used on C2.  Same time, less traffic
+      // (profiles/r5b_ab.txt).
+      if (t.len > 16) {
+        fa1 = LGS_RING_FAR_LD16(sp + 16);
+        if (t.len > 32) {
+          fa2 = LGS_RING_FAR_LD16(sp + 32);
+          if (t.len > 48) fa3 = LGS_RING_FAR_LD16(sp + 48);
+        }
+      }
     }
   };
 
   // Rotated: the loop's test is its last step (a test at the top became a
   // selector variable and a bool round trip through a VGPR).  A trip with no
   // active lane (every block's header corrupt) does nothing.
-#ifdef LGS_PROBE_TRIPCOUNT
-  uint32_t trips = 0;   // probe build (tools/ring_trips.py): trips of this wave
-#endif
+  LGS_RING_TRIPS_DECL;
+  LGS_RING_PH_DECL;
   do {
-#ifdef LGS_PROBE_TRIPCOUNT
-    ++trips;
-#endif
+    LGS_RING_TRIP();
+    LGS_RING_PH_TRIP();
+    LGS_RING_PH(7);                    // (the loop test, from the last trip)
 
     // ---- one piece of the current op for every lane whose bytes are in LDS;
     // this runs before the wait, so last trip's loads land meanwhile.
     piece();
     order();
+    LGS_RING_PH(0);
 
     // ---- everything issued last trip has landed: far-copy pieces (never
     // overlapping, <= 64 bytes), then the input refills.
     __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+    LGS_RING_PH(1);
     if ((st == 1) & (orem > 0) & ofar) {
       out_put(ob, made, fa0);
       if (orem > 16) out_put(ob, made + 16, fa1);
@@ -869,6 +873,7 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
     if (rm1 != sink) lwr16(s_in + rm1, rv1);
     order();
     in_have = in_req;
+    LGS_RING_PH(2);
 
     // ---- flush finished bytes; the block's last ones once the stream is
     // consumed (snappy.c:337: it must end exactly at want).
@@ -896,40 +901,49 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
         s_job[j] = RingJob(lane, F, fcnt, dp);
       }
       order();
+      // 4 lanes a job, 32 bytes each (bytes 16w.. and 64 + 16w..): 16 jobs
+      // per round, so a trip's flush is one round of two LDS round trips
+      // (a job record, then the ring) whenever at most 16 blocks flush.
+      // (8 lanes a job, 8 jobs a round: 274 against 268 us on C2,
+      // profiles/r5e_ab.txt.)
 #pragma clang loop unroll(disable)
-      for (uint32_t base = 0; base < total; base += 8) {
-        const uint32_t jj = base + (lane >> 3), w = lane & 7u;
-        // jj < base + 8 <= kJobs: the record is in range (stale past total).
+      for (uint32_t base = 0; base < total; base += 16) {
+        const uint32_t jj = base + (lane >> 2), w = lane & 3u;
+        // jj < base + 16 <= kJobs: the record is in range (stale past total).
         const RingJob jb = s_job[jj];
         if ((jj < total) & (16 * w < jb.cnt)) {
-          const u32x4 v = lrd16(s_out + (jb.lane() & (BL - 1)) * kOutStride + 16 +
-                                ((uint32_t)jb.ptr() & 15u) + ((jb.off + 16 * w) & (kOutRing - 1)));
-          const gptr<uint8_t> g =
-              (gptr<uint8_t>)jb.ptr() + jb.off + 16 * w;
-#ifndef LGS_PROBE_NOFLUSH
-          if (16 * w + 16 <= jb.cnt) st16(g, v);
-          else st_exact(g, v, jb.cnt - 16 * w);
-#else
-          if (v.x == 0x12345678u && jb.cnt == 77777u) st16(g, v);   // (never: keeps v live)
-#endif
+          const uint8_t* rb = s_out + (jb.lane() & (BL - 1)) * kOutStride + 16 +
+                              ((uint32_t)jb.ptr() & 15u);
+          const u32x4 v0 = lrd16(rb + ((jb.off + 16 * w) & (kOutRing - 1)));
+          const bool two = 64 + 16 * w < jb.cnt;
+          u32x4 v1 = v0;
+          if (two) v1 = lrd16(rb + ((jb.off + 64 + 16 * w) & (kOutRing - 1)));
+          const gptr<uint8_t> g = (gptr<uint8_t>)jb.ptr() + jb.off + 16 * w;
+          LGS_RING_FLUSH_ST(g, v0, jb.cnt - 16 * w);
+          if (two) LGS_RING_FLUSH_ST(g + 64, v1, jb.cnt - 64 - 16 * w);
         }
       }
       order();
       if (need) F += fcnt;
     }
+    LGS_RING_PH(3);
 
     // ---- parse the next tag.  TWO: then a second op slot -- its piece, if
     // its bytes are in LDS, and the tag after it.
     parse(false);
+    LGS_RING_PH(4);
     if (TWO) {
       order();
       piece();
       order();
       parse(true);
     }
+    LGS_RING_PH(5);
 
     // ---- refill requests: the next 64 input bytes, once the 64 they
-    // overwrite in the ring are consumed.  4 lanes per request, <= 32 a trip.
+    // overwrite in the ring are consumed.
+    // 4 lanes per request, <= 32 a trip.  (Each lane loading its own
+    // block's 64 bytes instead: the same time, profiles/r5f_ab.txt.)
     {
       const uint32_t cons = ((orem > 0) & (okind == 0)) ? olp : pos;
       const bool need = (st == 1) & (in_req < slen) & (in_req <= cons + 64);
@@ -966,15 +980,12 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
       order();
       if (need & (j < 32)) in_req += 64;
     }
+    LGS_RING_PH(6);
   } while (ballot(st == 1) & ~(ballot(orem == 0) & ballot(pos >= slen) & ballot(F >= made)));
 
   if (exists) {
     status[i] = (uint8_t)st;
-#ifdef LGS_PROBE_TRIPCOUNT
-    out_len[i] = trips;
-#else
-    out_len[i] = st == 1 ? want : 0;
-#endif
+    out_len[i] = LGS_RING_PH_VALUE(lane, LGS_RING_OUT_LEN(st == 1 ? want : 0));
   }
 }
 

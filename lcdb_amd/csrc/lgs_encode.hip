@@ -32,6 +32,7 @@
 //    every 64 ops flush_ops writes the literals and copy tags lane-parallel,
 //    a wave scan placing them, straight to the output slot.
 #include "lgs_device.h"
+#include "lgs_probe_hooks.h"
 #include "lgs_launch.h"
 
 namespace lgs {
@@ -567,13 +568,8 @@ __device__ __forceinline__ uint32_t encode_chunk(IN& x, uint32_t n, uint16_t* ta
     prev = (old >> sh) & 0xffffu;
     Raw32 yr = x.raw32(prev);                                     // the candidate's bytes
     // (Checked under the read's latency; the rare path reads them again.)
-#ifdef LGS_PROBE_FORCE_REPLAY
-    // Probe build (tools/probe_ab.py): every batch takes the replay path, so
-    // the path that never runs on gfx950 is checked against the reference.
-    if (vmask) {
-#else
-    if (ballot(prev > p) & vmask) {
-#endif
+    // (A probe build takes this path on every batch, lgs_probe_hooks.h.)
+    if (LGS_ENC_REPLAY(prev > p, vmask)) {
       // Not in lane order (never seen on gfx950): put back each touched
       // slot's entry as the batch found it (the one lane per slot that
       // received a value from before the batch), then swap lane by lane.
@@ -761,12 +757,7 @@ __global__ __launch_bounds__(64) void encode_kernel(
   const gptr<const uint8_t> src = to_global(in) + ioff;
   const OutSlot o = out_slot(out, ooff, len);
 
-#ifdef LGS_PROBE_ENC_TIMING
-  // probe (tools/enc_phases.py): shader-clock stamps of this wave's phases,
-  // stored in the last 16 bytes of its output slot (past the encoding)
-  const uint64_t tp0 = __builtin_amdgcn_s_memtime();
-  uint64_t tp1 = tp0;
-#endif
+  LGS_ENC_PH_DECL;
   uint32_t op = emit_header(o, hv);
 
   // snappy.c:370-381: independent 64 KiB chunks, a short tail as a literal.
@@ -780,10 +771,7 @@ __global__ __launch_bounds__(64) void encode_kernel(
     stage_in_linear<kR>(s.img, src + c0, clen);
     LdsIn x{s.img};
     order();
-#ifdef LGS_PROBE_ENC_TIMING
-    __builtin_amdgcn_s_waitcnt(0);
-    tp1 = __builtin_amdgcn_s_memtime();
-#endif
+    LGS_ENC_PH_STAGED();
     if (clen >= kMinBlock) {
       op = encode_chunk<kImg>(x, clen, s.tab, o, op, pl);
     } else {
@@ -791,16 +779,7 @@ __global__ __launch_bounds__(64) void encode_kernel(
     }
     order();
   }
-#ifdef LGS_PROBE_ENC_TIMING
-  __builtin_amdgcn_s_waitcnt(0);
-  const uint64_t tp2 = __builtin_amdgcn_s_memtime();
-  if (lane == 0) {
-    const uint32_t b = 32 + len + len / 6 - 16;
-    o.put4(0, b, (uint32_t)(tp1 - tp0));
-    o.put4(0, b + 4, (uint32_t)(tp2 - tp1));
-    o.put4(0, b + 8, 0x7e57u);
-  }
-#endif
+  LGS_ENC_PH_END(o, len);
   if (lane == 0) out_len[i] = op;
 }
 

@@ -11,6 +11,7 @@ for spec in "$@"; do
   name="${spec%%:*}"; flags="${spec#*:}"
   # shellcheck disable=SC2086
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -pthread \
+    -mllvm -phi-node-folding-threshold=8 -mllvm -two-entry-phi-node-folding-threshold=16 \
     -Wl,--version-script=lcdb_amd/csrc/exports.map $flags "${args[@]}" -o "probes/$name.so" &
   pids+=($!)
 done
