@@ -73,6 +73,8 @@ def parse(argv=None) -> argparse.Namespace:
                    help="skip the 1 GiB copy that measures the achievable HBM rate")
     p.add_argument("--no-pipelined", action="store_true",
                    help="skip the extra concurrent encode||decode measurement")
+    p.add_argument("--no-table", action="store_true",
+                   help="skip the batched table write/read extra field")
     p.add_argument("--no-c3", action="store_true",
                    help="skip the extra C3 (mixed 4/16/64 KiB) measurement at N = 1")
     p.add_argument("--c3-scale", type=int, default=32,
@@ -305,6 +307,34 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
                      "ms_per_step": tp / a.steps * 1e3,
                      "note": "encode(step k) || decode(step k-1) on two streams; extra field, "
                              "not value"}
+        # The same on disjoint CU sets (hipExtStreamCreateWithCUMask), sized by
+        # the two kernels' C2 times (~2:1): each kernel keeps its own LDS
+        # occupancy instead of the two thrashing each other's.
+        cu = cu_partition_streams(dev_index)
+        if cu is not None:
+            s_enc, s_dec, split = cu
+            batch.encode(raws[0], comps[0], s_enc)
+            enc_done[0].record(s_enc)
+            torch.cuda.synchronize()
+            if dist:
+                dist.barrier()
+            t0p = time.perf_counter()
+            for k in range(1, a.steps + 1):
+                j, jp = k % a.copies, (k - 1) % a.copies
+                if k >= a.copies:
+                    s_enc.wait_event(dec_done[j])
+                batch.encode(raws[j], comps[j], s_enc)
+                enc_done[j].record(s_enc)
+                s_dec.wait_event(enc_done[jp])
+                batch.decode(comps[jp], outs[jp], stats[jp], s_dec)
+                dec_done[jp].record(s_dec)
+            torch.cuda.synchronize()
+            tp = shard.max_over_ranks(time.perf_counter() - t0p, dist)
+            pipelined["cu_partition"] = {
+                "GiBps": raw_bytes * world * a.steps / tp / 2**30,
+                "ms_per_step": tp / a.steps * 1e3, "cus_encode_decode": split,
+                "note": "encode and decode streams on disjoint CU sets (CU i -> decode when "
+                        "i % 3 == 2)"}
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
@@ -385,6 +415,13 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
     if rank == 0 and not a.no_cpu_baseline:
         cpu = cpu_baseline(c, a, hc, world)
 
+    # ---- extra (not `value`): SURVEY §8(f) rows 2-3 on the same C2 blocks,
+    # the batched table write (encode + 12.5 % rule + trailers + packing)
+    # and read (truncation + checksums + decode), against the codec kernels.
+    tables = None
+    if world == 1 and not a.no_table:
+        tables = table_paths(c, raws[0], stream, enc_ms, dec_ms)
+
     # ---- extra (not `value`): BASELINE.json configs[2] on this GPU, after
     # everything above, with its own buffers (the C2 ones are freed first).
     c3 = None
@@ -415,10 +452,93 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
             "encode_GiBps": raw_bytes * world / (enc_ms * 1e-3) / 2**30,
             "decode_GiBps": raw_bytes * world / (dec_ms * 1e-3) / 2**30,
             "kernels": kern, "roofline": roof, "cpu_baseline": cpu, "parity": parity,
-            "pipelined": pipelined, "c3": c3,
+            "pipelined": pipelined, "c3": c3, "table": tables,
             "gen_seconds": t_gen,
         }
         print(json.dumps(line), flush=True)
+
+
+def table_paths(c, raw, stream, enc_ms: float, dec_ms: float) -> dict:
+    """lgs_table_write_dev / lgs_table_read_dev (verify_checksums on) over the
+    C2 blocks, buffers allocated once, HIP events on the launch stream, median
+    of 10 after 2 warm-ups; the read-back is checked against the raw blocks."""
+    import torch
+    from lcdb_amd import batch, table
+    n = c.n
+    raw_bytes = c.raw_bytes
+    max_len = int(c.len.max())
+
+    def timed(fn) -> float:
+        ts = []
+        for k in range(12):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            if k >= 2:
+                ts.append(e0.elapsed_time(e1))
+        return float(np.median(ts))
+
+    bufs = table.write_buffers(n, raw_bytes, raw.buf.device)
+    w_ms = timed(lambda: table.write_blocks(raw.buf, raw.off, raw.len, 1, 0, max_len, raw_bytes,
+                                            stream, bufs))
+    d_file, hoff, hsize, end, _ = bufs
+    file_len = int(end.cpu()[0])
+    dec = batch.decode_slots(c.len, raw.buf.device)
+    olen = torch.zeros(n, dtype=torch.int32, device=raw.buf.device)
+    st = torch.zeros(n, dtype=torch.uint8, device=raw.buf.device)
+    scr = torch.empty(max(int(table._L.lgs_table_read_scratch(n)), 1), dtype=torch.uint8,
+                      device=raw.buf.device)
+    r_ms = timed(lambda: table.read_blocks(d_file, file_len, hoff, hsize, dec.buf, dec.off,
+                                           dec.cap, dec.max_cap, True, olen, st, stream, scr))
+    ok = bool((st == 1).all()) and torch.equal(olen, raw.len)
+    ho = batch.to_host(dec)
+    ho.len = olen.cpu().numpy().astype(np.uint32)
+    ok = ok and np.array_equal(corpus_digests(ho), corpus_digests(c))
+    res = {"workload": f"C2 framing: {n} blocks, device-resident, verify_checksums on",
+           "file_bytes": file_len,
+           "write_ms": w_ms, "write_GiBps_raw": raw_bytes / (w_ms * 1e-3) / 2**30,
+           "read_ms": r_ms, "read_GiBps_raw": raw_bytes / (r_ms * 1e-3) / 2**30,
+           "write_over_encode": w_ms / enc_ms, "read_over_decode": r_ms / dec_ms,
+           "parity": "write -> read round trip exact, every checksum verified" if ok
+                     else "MISMATCH",
+           "note": "extra field (SURVEY §8(f) rows 2-3), not value"}
+    del bufs, d_file, dec, scr
+    torch.cuda.empty_cache()
+    return res
+
+
+def corpus_digests(c):
+    from lcdb_amd import corpus
+    return corpus.block_digests(c.buf, c.off, c.len)
+
+
+def cu_partition_streams(dev_index: int):
+    """Two HIP streams on disjoint CUs of this GPU: encode gets CUs i with
+    i % 3 != 2, decode the rest (the kernels' C2 times are ~2:1).  Returns
+    (encode stream, decode stream, [n_encode_cus, n_decode_cus]) as torch
+    ExternalStreams, or None where the runtime refuses the mask."""
+    import ctypes as C
+    import torch
+    try:
+        hip = C.CDLL("libamdhip64.so")
+    except OSError:
+        return None
+    ncu = torch.cuda.get_device_properties(dev_index).multi_processor_count
+    words = (ncu + 31) // 32
+    enc, dec = [0] * words, [0] * words
+    for i in range(ncu):
+        (dec if i % 3 == 2 else enc)[i // 32] |= 1 << (i % 32)
+    out = []
+    for m in (enc, dec):
+        s = C.c_void_p()
+        if hip.hipExtStreamCreateWithCUMask(C.byref(s), C.c_uint32(words),
+                                            (C.c_uint32 * words)(*m)) != 0:
+            return None
+        out.append(torch.cuda.ExternalStream(s.value, device=torch.device("cuda", dev_index)))
+    return out[0], out[1], [sum(bin(x).count("1") for x in enc),
+                            sum(bin(x).count("1") for x in dec)]
 
 
 def c3_mixed(a, dev, stream) -> dict:

@@ -29,14 +29,15 @@ PROBE_SOURCES = ["lgs_decode_probe.hip", "lgs_decode_group.hip", "lgs_decode_cha
 
 HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip",
                "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp", "lgs_probe.hip"]
-HIP_HEADERS = ["lgs_device.h", "lgs_launch.h", "lgs_decode_common.h"]
+HIP_HEADERS = ["lgs_device.h", "lgs_launch.h", "lgs_decode_common.h", "lgs_probe_hooks.h",
+               "lgs_service.h"]
 # Only ldb_snappy_* and lgs_* are exported (the library is loaded into lcdb).
 EXPORTS_MAP = os.path.join(CSRC, "exports.map")
 # The files that define the two profiled codec kernels and how they are
 # launched (grid, LDS class, split); the host runtime, table and bloom
 # sources do not change what encode_kernel / decode_ring_kernel execute.
 CODEC_KERNEL_FILES = ["lgs_encode.hip", "lgs_decode.hip", "lgs_device.h", "lgs_launch.h",
-                      "lgs_decode_common.h"]
+                      "lgs_decode_common.h", "lgs_probe_hooks.h", "lgs_service.h"]
 ARCH = "gfx950"
 # If-conversion thresholds: hipcc's defaults leave small two-way branches as
 # exec-mask regions; these fold them into selects (the ring decoder's trip:

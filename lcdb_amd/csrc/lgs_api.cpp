@@ -167,6 +167,8 @@ struct Ctx {
   size_t h_cap = 0;
   uint8_t* h_dev = nullptr; // a drop-in slot's pinned arena as the device sees it
   bool fixed = false;       // a drop-in slot: arenas never grow
+  uint32_t svc_idx = ~0u;   // a drop-in slot's service mailbox (kSvcMaxSlots: none)
+  uint32_t svc_seq[2] = {0, 0};   // its last request per kind (encode, decode)
 };
 
 // lgs_set_device() choice of the calling thread (-1: its current device).
@@ -307,6 +309,7 @@ class CtxPool {
     }
     std::lock_guard<std::mutex> g(mu_);
     all_.push_back(c);
+    if (fixed_cap_) c->svc_idx = next_idx_[c->device]++;
     return LGS_OK;
   }
   static void destroy_partial(Ctx* c) {
@@ -330,6 +333,7 @@ class CtxPool {
   std::vector<Ctx*> free_[64];
   unsigned live_[64] = {};
   std::vector<Ctx*> all_;
+  uint32_t next_idx_[64] = {};
 };
 
 CtxPool& dropin_pool() {
@@ -497,6 +501,167 @@ int read_varint32(uint32_t* v, const uint8_t* p, size_t n) {
 // into it, launches the kernel on it (input read and output written over
 // PCIe, no hipMemcpy) and synchronises once.
 
+// ---- the drop-in service (lgs_launch.h, lgs_service.h) ----
+//
+// One request at a time per slot: the input goes to the slot's arena at
+// kSvcIn, {sequence, length} into its mailbox with one 8-byte store, and the
+// call spins on the mailbox's ack (host memory) until the resident wave has
+// written the output at kSvcOut.  The service kernels start on the first
+// request; a request that finds its kernel gone (idle exit) relaunches it.
+// LGS_DROPIN_SERVICE=0 (or lgs_set_option("service", "0")) sends every call
+// through the launch path instead; so do items over kSvcMaxItem.
+std::atomic<int> g_svc_enabled{[] {
+  const char* e = getenv("LGS_DROPIN_SERVICE");
+  return e && !strcmp(e, "0") ? 0 : 1;
+}()};
+std::atomic<bool> g_svc_shutdown{false};
+
+// Idle exit of the resident waves (LGS_SERVICE_IDLE_US, default 2 ms): a
+// device-wide synchronisation waits at most this long after the last call.
+uint64_t svc_idle_us() {
+  static const uint64_t v = env_size("LGS_SERVICE_IDLE_US", 2000, 50, 10000000);
+  return v;
+}
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+struct Service {
+  std::mutex mu;
+  int state = 0;                      // 0 not set up, 1 ready, -1 unavailable
+  SvcMailbox* mb = nullptr;           // host view: encode [0, S), decode [S, 2S)
+  SvcMailbox* mb_dev = nullptr;
+  uint64_t* activity = nullptr;       // device, one u64 per kind
+  hipStream_t stream[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  std::atomic<bool> launched[2];
+  std::atomic<int64_t> last_use[2];   // steady-clock ns of the last finished request
+  uint32_t nslots = 0;
+
+  SvcMailbox* box(int kind, uint32_t idx) { return mb + (size_t)kind * kSvcMaxSlots + idx; }
+
+  int setup() {                       // under mu
+    if (state) return state > 0 ? LGS_OK : LGS_EINTERNAL;
+    state = -1;
+    const size_t bytes = 2 * kSvcMaxSlots * sizeof(SvcMailbox);
+    if (hipHostMalloc(&mb, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(LGS_ENOMEM, "service mailboxes: hipHostMalloc(%zu) failed", bytes);
+    memset(mb, 0, bytes);
+    void* dp = nullptr;
+    LGS_HIP(hipHostGetDevicePointer(&dp, mb, 0));
+    mb_dev = (SvcMailbox*)dp;
+    if (hipMalloc(&activity, 16) != hipSuccess) return fail(LGS_ENOMEM, "service: hipMalloc failed");
+    LGS_HIP(hipMemset(activity, 0, 16));
+    for (int k = 0; k < 2; ++k) {
+      LGS_HIP(hipStreamCreateWithFlags(&stream[k], hipStreamNonBlocking));
+      LGS_HIP(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+      last_use[k] = 0;
+      launched[k] = false;
+    }
+    const unsigned s = dropin_max_slots();
+    nslots = s < kSvcMaxSlots ? s : kSvcMaxSlots;
+    state = 1;
+    return LGS_OK;
+  }
+
+  // The kernel of `kind` running, or (re)launched.  check: ask the runtime
+  // whether a launched kernel has exited (idle) even if it was seen running.
+  int ensure(int kind) {
+    std::lock_guard<std::mutex> g(mu);
+    if (launched[kind]) {
+      const hipError_t q = hipEventQuery(done[kind]);
+      // (A pending query's hipErrorNotReady must not linger as this thread's
+      // last error: the launchers return hipGetLastError().)
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return LGS_OK;
+      }
+      if (q != hipSuccess) LGS_HIP(q);
+    }
+    const uint64_t idle = svc_idle_us() * 100;          // 100 MHz ticks
+    LGS_HIP(kind == 0 ? launch_encode_service(mb_dev, nslots, idle, activity, stream[0])
+                      : launch_decode_service(mb_dev + kSvcMaxSlots, nslots, idle, activity + 1,
+                                              stream[1]));
+    LGS_HIP(hipEventRecord(done[kind], stream[kind]));
+    launched[kind] = true;
+    return LGS_OK;
+  }
+};
+
+Service* g_services[64] = {};
+std::mutex g_services_mu;
+
+void svc_stop_all() {
+  g_svc_shutdown = true;
+  for (Service* sv : g_services)
+    if (sv && sv->state > 0)
+      for (uint32_t i = 0; i < 2 * kSvcMaxSlots; ++i)
+        __atomic_store_n(&sv->mb[i].stop, 1u, __ATOMIC_RELEASE);
+}
+
+// The calling slot's service, ready, with its arena registered; nullptr
+// when the call should take the launch path.
+Service* svc_for(Ctx& c) {
+  if (!g_svc_enabled.load(std::memory_order_relaxed) || g_svc_shutdown.load() ||
+      c.svc_idx >= kSvcMaxSlots || c.device < 0 || c.device >= 64)
+    return nullptr;
+  Service* sv;
+  {
+    std::lock_guard<std::mutex> g(g_services_mu);
+    sv = g_services[c.device];
+    if (!sv) {
+      sv = g_services[c.device] = new Service;
+      static std::once_flag once;
+      std::call_once(once, [] { atexit(svc_stop_all); });
+    }
+  }
+  std::lock_guard<std::mutex> g(sv->mu);
+  if (sv->setup() != LGS_OK) return nullptr;
+  if (c.svc_idx >= sv->nslots) return nullptr;
+  for (int k = 0; k < 2; ++k) {
+    SvcMailbox* m = sv->box(k, c.svc_idx);
+    if (__atomic_load_n(&m->arena, __ATOMIC_RELAXED) == 0)
+      __atomic_store_n(&m->arena, (uint64_t)(uintptr_t)c.h_dev, __ATOMIC_RELEASE);
+  }
+  return sv;
+}
+
+// Post the request already staged at kSvcIn and wait for it: *status and
+// *out_len as the wave reported them.
+int svc_call(Service& sv, Ctx& c, int kind, uint32_t len, uint32_t* status, uint32_t* out_len) {
+  SvcMailbox* m = sv.box(kind, c.svc_idx);
+  uint32_t seq = c.svc_seq[kind] + 1;
+  if (seq == 0) seq = 1;
+  c.svc_seq[kind] = seq;
+  __atomic_store_n(reinterpret_cast<uint64_t*>(m), (uint64_t)seq | ((uint64_t)len << 32),
+                   __ATOMIC_RELEASE);
+  const int64_t t_post = now_ns();
+  // Not used for over half the idle time: its kernel has likely exited.
+  if (!sv.launched[kind] ||
+      t_post - sv.last_use[kind].load(std::memory_order_relaxed) > (int64_t)svc_idle_us() * 500)
+    LGS_TRY(sv.ensure(kind));
+  int64_t t_check = t_post;
+  for (uint32_t spin = 0; __atomic_load_n(&m->ack, __ATOMIC_ACQUIRE) != seq; ++spin) {
+    __builtin_ia32_pause();
+    if ((spin & 255) == 255) {
+      const int64_t t = now_ns();
+      if (t - t_check > 50000) {                     // 50 us: is the kernel still there?
+        LGS_TRY(sv.ensure(kind));
+        t_check = t;
+      }
+      if (t - t_post > 20000000000ll)
+        return fail(LGS_EINTERNAL, "drop-in service: no answer in 20 s");
+    }
+  }
+  *status = __atomic_load_n(&m->status, __ATOMIC_RELAXED);
+  *out_len = __atomic_load_n(&m->out_len, __ATOMIC_RELAXED);
+  sv.last_use[kind].store(now_ns(), std::memory_order_relaxed);
+  return LGS_OK;
+}
+
 // Device bytes one 64 KiB-or-less chunk takes in a pass.
 constexpr size_t kChunkIn = kChunk + 16;                         // its input
 size_t chunk_out(uint32_t len) { return align_up(bound_of(len) + 8, 16); }
@@ -507,6 +672,19 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
   LGS_TRY(lease.acquire());
   Ctx& c = lease.ctx();
   const uint32_t n = (uint32_t)xn;
+  if (n <= kSvcMaxItem) {
+    if (Service* sv = svc_for(c)) {                              // a resident wave
+      memcpy(c.h_buf + kSvcIn, xp, n);
+      memset(c.h_buf + kSvcIn + n, 0, 16);
+      uint32_t st = 0, olen = 0;
+      LGS_TRY(svc_call(*sv, c, 0, n, &st, &olen));
+      if (st != 1 || olen > bound_of(n))
+        return fail(LGS_EINTERNAL, "service encode: status %u, %u bytes", st, olen);
+      memcpy(zp, c.h_buf + kSvcOut, olen);
+      *written = olen;
+      return LGS_OK;
+    }
+  }
   // snappy.c:370-381: full 64 KiB chunks, then the remainder (if any);
   // a zero-length input is one empty item (just the varint header).
   const uint32_t nit = n <= kChunk ? 1u : (n + kChunk - 1) / kChunk;
@@ -646,6 +824,19 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   LGS_TRY(lease.acquire());
   Ctx& c = lease.ctx();
   uint8_t* const h = c.h_buf;
+  if (want <= kSvcMaxItem && (size_t)n + 16 <= kSvcOut - kSvcIn) {
+    if (Service* sv = svc_for(c)) {                              // a resident wave
+      memcpy(h + kSvcIn, xp, n);
+      memset(h + kSvcIn + n, 0, 16);
+      uint32_t st = 0, olen = 0;
+      LGS_TRY(svc_call(*sv, c, 1, n, &st, &olen));
+      if (st == LGS_ST_OK && olen != want)
+        return fail(LGS_EINTERNAL, "service decode: %u bytes for a %u-byte header", olen, want);
+      if (st == LGS_ST_OK) memcpy(zp, h + kSvcOut, want);
+      *ok = st == LGS_ST_OK;
+      return LGS_OK;
+    }
+  }
 
   Layout L;
   const size_t o_in = L.take((size_t)n + 16);
@@ -738,6 +929,18 @@ Options& options_init() {
     if (dk && !strcmp(dk, "ops")) v->decoder = kDecOps;
     const char* wd = getenv("LGS_WIDE_DECODER");
     if (wd && !strcmp(wd, "trips")) v->wide = kWideTrips;
+#endif
+#ifndef LGS_PROBE_DECODERS
+    // The decoders that lost their A/B exist in the probe library only: say
+    // so rather than silently measuring the default.
+    const char* wd0 = getenv("LGS_WIDE_DECODER");
+    if ((dk && (!strcmp(dk, "quad") || !strcmp(dk, "ops") || !strcmp(dk, "group") ||
+                !strcmp(dk, "chain"))) ||
+        (wd0 && (!strcmp(wd0, "trips") || !strcmp(wd0, "group"))))
+      fprintf(stderr,
+              "lcdb_gpu_snappy: LGS_DECODE_KERNEL=%s LGS_WIDE_DECODER=%s names a probe-library "
+              "decoder; this library uses its default decoders\n",
+              dk ? dk : "", wd0 ? wd0 : "");
 #endif
     const char* ns = getenv("LGS_NO_SPLIT");
     if (ns && *ns && strcmp(ns, "0")) v->split = 0;
@@ -838,6 +1041,12 @@ int lgs_set_option(const char* name, const char* value) {
     else if (!strcmp(value, "trips")) o.wide = kWideTrips;
 #endif
     else return fail(LGS_EINVAL, "wide '%s' (walk)", value);
+    return LGS_OK;
+  }
+  if (!strcmp(name, "service")) {   // the drop-in's resident waves (LGS_DROPIN_SERVICE)
+    if (!strcmp(value, "1")) g_svc_enabled = 1;
+    else if (!strcmp(value, "0")) g_svc_enabled = 0;
+    else return fail(LGS_EINVAL, "service '%s' (0 or 1)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "split")) {

@@ -22,6 +22,7 @@
 #include "lgs_decode_common.h"
 #include "lgs_launch.h"
 #include "lgs_probe_hooks.h"
+#include "lgs_service.h"
 
 #include <mutex>
 
@@ -209,6 +210,48 @@ __device__ uint32_t decode_win(const uint8_t* base, uint32_t sh, uint32_t slen, 
   return made == want ? 1u : 0u;                    // snappy.c:337
 }
 
+// One in-place buffer per wave: the output image grows from the bottom, the
+// compressed stream is staged at the top (+ 48 for its alignment shift and
+// zero pad, + 256 so the window reads of decode_win never read past the
+// array).  kMargin is how far the output may run ahead of the input (literal
+// headers still unread); half the LDS of separate input and output images,
+// so twice the waves per CU.
+template <uint32_t OUT_CAP>
+struct DecBuf {
+  static constexpr uint32_t kMargin = 512 + OUT_CAP / 64;
+  static constexpr uint32_t kBuf = (OUT_CAP + 32 + kMargin + 48 + 256 + 15) & ~15u;
+};
+
+// One block: the stream src[0 .. slen) decoded into dst (capacity cap),
+// built in the wave's LDS buffer buf (DecBuf<OUT_CAP>::kBuf bytes).  Returns
+// the status (1 ok, 0 corrupt, 2 no space), *want_out the decoded length.
+template <uint32_t OUT_CAP>
+__device__ __forceinline__ uint32_t decode_item(uint8_t* buf, gptr<const uint8_t> src,
+                                                uint32_t slen, gptr<uint8_t> dst, uint32_t cap0,
+                                                uint32_t* want_out) {
+  constexpr uint32_t kBuf = DecBuf<OUT_CAP>::kBuf;
+  LGS_DEC_PH_DECL;
+  const uint32_t cap = cap0 < OUT_CAP ? cap0 : OUT_CAP;
+  const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
+  uint8_t* o = buf + oshift;
+
+  uint32_t want = 0, st = 3;
+  if (slen <= kBuf - 48 - 256) {
+    const uint32_t ib = (kBuf - slen - 48 - 256) & ~15u;
+    constexpr uint32_t kR = (kBuf + 1023) / 1024 < 8 ? (kBuf + 1023) / 1024 : 8;
+    const uint32_t sh = stage_in<kR>(buf + ib, src, slen);
+    order();
+    LGS_DEC_PH_STAGED();
+    st = decode_win(buf + ib, sh, slen, o, (int32_t)ib - (int32_t)oshift, cap, &want);
+    order();
+    LGS_DEC_PH_END(flush_out(dst, buf, want), (gptr<uint32_t>)(dst + ((cap0 - 16) & ~3u)));
+  }
+  if (st == 3) st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
+  if (st == 1) flush_out(dst, buf, want);
+  *want_out = want;
+  return st;
+}
+
 template <uint32_t OUT_CAP, uint32_t WAVES>
 __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -217,15 +260,7 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
     uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
     const uint32_t* __restrict__ index, uint32_t n,
     const uint32_t* __restrict__ count, const Item1 one) {
-  // One in-place buffer per wave: the output image grows from the bottom,
-  // the compressed stream is staged at the top (+ 48 for its alignment
-  // shift and zero pad, + 256 so the window reads of decode_win never read
-  // past the array).  kMargin is how far the output may run ahead of the
-  // input (literal headers still unread); half the LDS of separate
-  // input and output images, so twice the waves per CU.
-  constexpr uint32_t kMargin = 512 + OUT_CAP / 64;
-  constexpr uint32_t kBuf = (OUT_CAP + 32 + kMargin + 48 + 256 + 15) & ~15u;
-  __shared__ __attribute__((aligned(16))) uint8_t s_buf[WAVES][kBuf];
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[WAVES][DecBuf<OUT_CAP>::kBuf];
 
   // Per-wave scalars go through v_readfirstlane so hipcc keeps the whole
   // tag walk on the SALU (it cannot prove threadIdx.x >> 6 wave-uniform).
@@ -234,7 +269,6 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   if (slot >= (count ? uni(*count) : n)) return;
   const uint32_t i = uni(index ? index[slot] : slot);
 
-  LGS_DEC_PH_DECL;
   uint64_t ioff, ooff;
   uint32_t slen, cap;
   if (one.on) {                                     // the drop-in's item, by value
@@ -242,30 +276,39 @@ __global__ __launch_bounds__(64 * WAVES) void decode_kernel(
   } else {
     ioff = uni64(in_off[i]); ooff = uni64(out_off[i]); slen = uni(in_len[i]); cap = uni(out_cap[i]);
   }
-  cap = cap < OUT_CAP ? cap : OUT_CAP;
-  const gptr<const uint8_t> src = to_global(in) + ioff;
-  const gptr<uint8_t> dst = to_global(out) + ooff;
-  const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
-  uint8_t* o = &s_buf[wv][oshift];
-
-  uint32_t want = 0, st = 3;
-  if (slen <= kBuf - 48 - 256) {
-    const uint32_t ib = (kBuf - slen - 48 - 256) & ~15u;
-    constexpr uint32_t kR = (kBuf + 1023) / 1024 < 8 ? (kBuf + 1023) / 1024 : 8;
-    const uint32_t sh = stage_in<kR>(&s_buf[wv][ib], src, slen);
-    order();
-    LGS_DEC_PH_STAGED();
-    st = decode_win(&s_buf[wv][ib], sh, slen, o, (int32_t)ib - (int32_t)oshift, cap, &want);
-    order();
-    LGS_DEC_PH_END(flush_out(dst, &s_buf[wv][0], want),
-                   (gptr<uint32_t>)(dst + ((out_cap[i] - 16) & ~3u)));
-  }
-  if (st == 3) st = decode_stream(GlobalStream{src, slen}, slen, o, cap, &want);
-  if (st == 1) flush_out(dst, &s_buf[wv][0], want);
+  uint32_t want = 0;
+  const uint32_t st = decode_item<OUT_CAP>(&s_buf[wv][0], to_global(in) + ioff, slen,
+                                           to_global(out) + ooff, cap, &want);
   if (lane_id() == 0) {
     status[i] = (uint8_t)st;
     out_len[i] = st == 1 ? want : 0;
   }
+}
+
+// The drop-in service's decode waves (lgs_launch.h): wave k serves mailbox
+// k, one stream whose output is <= kSvcMaxItem bytes at a time (the host
+// checked the header), from its slot's arena.
+__global__ __launch_bounds__(64) void decode_service_kernel(SvcMailbox* __restrict__ mb,
+                                                            uint64_t idle,
+                                                            uint64_t* __restrict__ activity) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[DecBuf<kSvcMaxItem>::kBuf];
+  svc_loop(mb + blockIdx.x, idle, activity,
+           [&](uint32_t len, uint64_t arena, uint32_t* status, uint32_t* out_len) {
+             uint8_t* a = reinterpret_cast<uint8_t*>(arena);
+             len = len < kSvcOut - kSvcIn - 16 ? len : kSvcOut - kSvcIn - 16;   // (never more)
+             uint32_t want = 0;
+             const uint32_t st = decode_item<kSvcMaxItem>(s_buf, to_global(a) + kSvcIn, len,
+                                                          to_global(a) + kSvcOut, kSvcMaxItem,
+                                                          &want);
+             *status = st;
+             *out_len = st == 1 ? want : 0;
+           });
+}
+
+hipError_t launch_decode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
+                                 uint64_t* activity, hipStream_t s) {
+  hipLaunchKernelGGL(decode_service_kernel, dim3(nslots), dim3(64), 0, s, mb, idle, activity);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -1156,6 +1199,8 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
 
 hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  // (As launch_encode: a by-value item only in a one-item launch.)
+  if (a.one.on && (a.n != 1 || a.index)) return hipErrorInvalidValue;
   const int force = options().decoder.load(std::memory_order_relaxed);
 #ifdef LGS_PROBE_DECODERS
   if (force == kDecOps && max_out <= kDecCap0) return launch_decode_ops(a, s);

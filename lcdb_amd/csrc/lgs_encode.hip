@@ -34,6 +34,7 @@
 #include "lgs_device.h"
 #include "lgs_probe_hooks.h"
 #include "lgs_launch.h"
+#include "lgs_service.h"
 
 namespace lgs {
 
@@ -726,37 +727,17 @@ struct EncLds {
 // 0xffffffff for none (a later chunk of a > 64 KiB block).  One wave per
 // work item, one-wave workgroups (a static partition over persistent waves
 // balances worse).
+// One block (or a > 64 KiB block's chunks, one after the other) of `len`
+// bytes at src, encoded into o with the varint header hv (0xffffffff: none).
+// s: the wave's LDS (the kernel's only __shared__ object, at LDS 0).
 template <uint32_t IN_CAP>
-__global__ __launch_bounds__(64) void encode_kernel(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
-    const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
-    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
-    const uint32_t* __restrict__ count, const Item1 one) {
+__device__ __forceinline__ uint32_t encode_item(EncLds<IN_CAP + 112>& s, gptr<const uint8_t> src,
+                                                uint32_t len, uint32_t hv, const OutSlot& o) {
   // Image: + 48 the zero granule past it (and spare), + 64 the match
   // extension's reads past the chunk (encode_chunk).  8 832 B with the
   // table: 18 waves per CU (the 1 280-byte LDS granule).
   constexpr uint32_t kImg = IN_CAP + 112;
-  __shared__ __attribute__((aligned(16))) EncLds<kImg> s;
-  if (lds_addr(&s) != 0) __builtin_trap();            // encode_chunk<kImg> assumes it
-
-  const uint32_t slot = blockIdx.x;
-  if (slot >= (count ? uni(*count) : n)) return;
-  const uint32_t i = uni(index ? index[slot] : slot);
-  const uint32_t lane = lane_id();
-  const PostLanes pl = post_lanes(lane);
-
-  uint64_t ioff, ooff;
-  uint32_t len, hv;
-  if (one.on) {                                     // the drop-in's item, by value
-    ioff = one.in_off; ooff = one.out_off; len = one.in_len; hv = one.aux;
-  } else {
-    ioff = uni64(in_off[i]); ooff = uni64(out_off[i]); len = uni(in_len[i]);
-    hv = uni(hdr ? hdr[i] : len);
-  }
-  const gptr<const uint8_t> src = to_global(in) + ioff;
-  const OutSlot o = out_slot(out, ooff, len);
-
+  const PostLanes pl = post_lanes(lane_id());
   LGS_ENC_PH_DECL;
   uint32_t op = emit_header(o, hv);
 
@@ -780,7 +761,62 @@ __global__ __launch_bounds__(64) void encode_kernel(
     order();
   }
   LGS_ENC_PH_END(o, len);
-  if (lane == 0) out_len[i] = op;
+  return op;
+}
+
+// Work item i: input in[in_off[i] .. + in_len[i]), output at out + out_off[i].
+// hdr == nullptr: item is a whole block, prefixed with its varint32 length
+// (snappy.c:368).  Otherwise hdr[i] is the varint value to prefix, or
+// 0xffffffff for none (a later chunk of a > 64 KiB block).  One wave per
+// work item, one-wave workgroups (a static partition over persistent waves
+// balances worse).
+template <uint32_t IN_CAP>
+__global__ __launch_bounds__(64) void encode_kernel(
+    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
+    const uint32_t* __restrict__ hdr, const uint32_t* __restrict__ index, uint32_t n,
+    const uint32_t* __restrict__ count, const Item1 one) {
+  __shared__ __attribute__((aligned(16))) EncLds<IN_CAP + 112> s;
+  if (lds_addr(&s) != 0) __builtin_trap();            // encode_chunk<kImg> assumes it
+
+  const uint32_t slot = blockIdx.x;
+  if (slot >= (count ? uni(*count) : n)) return;
+  const uint32_t i = uni(index ? index[slot] : slot);
+
+  uint64_t ioff, ooff;
+  uint32_t len, hv;
+  if (one.on) {                                     // the drop-in's item, by value
+    ioff = one.in_off; ooff = one.out_off; len = one.in_len; hv = one.aux;
+  } else {
+    ioff = uni64(in_off[i]); ooff = uni64(out_off[i]); len = uni(in_len[i]);
+    hv = uni(hdr ? hdr[i] : len);
+  }
+  const uint32_t op = encode_item<IN_CAP>(s, to_global(in) + ioff, len, hv, out_slot(out, ooff, len));
+  if (lane_id() == 0) out_len[i] = op;
+}
+
+// The drop-in service's encode waves (lgs_launch.h): wave k serves mailbox
+// k, one block of <= kSvcMaxItem bytes at a time, from its slot's arena.
+__global__ __launch_bounds__(64) void encode_service_kernel(SvcMailbox* __restrict__ mb,
+                                                            uint64_t idle,
+                                                            uint64_t* __restrict__ activity) {
+  __shared__ __attribute__((aligned(16))) EncLds<kSvcMaxItem + 112> s;
+  if (lds_addr(&s) != 0) __builtin_trap();
+  svc_loop(mb + blockIdx.x, idle, activity,
+           [&](uint32_t len, uint64_t arena, uint32_t* status, uint32_t* out_len) {
+             uint8_t* a = reinterpret_cast<uint8_t*>(arena);
+             len = len < kSvcMaxItem ? len : kSvcMaxItem;    // (the host never posts more)
+             *out_len = encode_item<kSvcMaxItem>(s, to_global(a) + kSvcIn, len, len,
+                                                 out_slot(a, kSvcOut, len));
+             *status = 1;
+           });
+}
+
+hipError_t launch_encode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
+                                 uint64_t* activity, hipStream_t s) {
+  hipLaunchKernelGGL(encode_service_kernel, dim3(nslots), dim3(64), 0, s, mb, idle, activity);
+  return hipGetLastError();
 }
 
 // The 64 KiB class with its chunk in a W-byte LDS ring (WinIn): 32 KiB +
@@ -858,6 +894,9 @@ static hipError_t launch_encode_big(const EncodeArgs& a, hipStream_t s) {
 // Blocks longer than 64 KiB are encoded chunk by chunk by their wave.
 hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
+  // A by-value item stands for item 0 of a one-item launch; with more items
+  // or an index list every slot would encode item 0.
+  if (a.one.on && (a.n != 1 || a.index)) return hipErrorInvalidValue;
   if (max_in <= kEncCap0) return launch_encode_small(a, s);
   if (a.index || a.n < kSplitMinBlocks || !options().split) {
     if (max_in <= kEncCap1) return launch_encode_cls<kEncCap1>(a, s);

@@ -111,6 +111,45 @@ class Scratch {
   hipError_t err_;
 };
 
+// ---- the drop-in service: resident encode / decode waves ----
+//
+// A drop-in call of one small block spends ~17 us on a kernel launch and a
+// stream synchronisation (profiles/r4z_dropin_breakdown.json).  The service
+// keeps one wave per drop-in slot resident instead: wave k of the encode (or
+// decode) service kernel polls mailbox k in the slot's mapped pinned memory,
+// runs the ordinary single-block walk on the slot's arena when the host posts
+// a request, and posts completion back.  A wave exits after `idle` 100 MHz
+// ticks without a request anywhere in its kernel (so a device-wide
+// synchronisation waits at most that long) or when the host sets its stop
+// flag; the host relaunches the kernel when a request finds it gone.
+constexpr uint32_t kSvcMaxSlots = 64;      // mailboxes per kind
+constexpr uint32_t kSvcMaxItem = 4608;     // the 4 KiB LDS class (encode input / decode output)
+constexpr uint32_t kSvcIn = 0;             // arena offset of the request's input
+constexpr uint32_t kSvcOut = 8192;         // arena offset of its output (>= 16 + bound(4608))
+
+struct alignas(128) SvcMailbox {
+  // host -> device: one 16-byte group (read in one request) + the arena
+  uint32_t req;      // sequence number of the posted request
+  uint32_t len;      // input bytes at arena + kSvcIn
+  uint32_t aux;      // encode: the varint header value; decode: the output capacity
+  uint32_t stop;     // nonzero: the wave exits
+  uint64_t arena;    // device address of the slot's mapped arena
+  uint64_t pad0[5];
+  // device -> host
+  uint32_t ack;      // sequence number of the last finished request
+  uint32_t status;   // decode: LGS_ST_*; encode: 1
+  uint32_t out_len;  // bytes written at arena + kSvcOut
+  uint32_t pad1[13];
+};
+static_assert(sizeof(SvcMailbox) == 128, "mailbox layout");
+
+// nslots waves polling mb[0 .. nslots); activity: 8 bytes of device memory
+// shared by the kernel's waves (their last request, in 100 MHz ticks).
+hipError_t launch_encode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
+                                 uint64_t* activity, hipStream_t s);
+hipError_t launch_decode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
+                                 uint64_t* activity, hipStream_t s);
+
 // ---- SSTable block framing (lgs_table.hip) ----
 
 // Per-block status codes (the LGS_ST_* values of include/lcdb_gpu_snappy.h).

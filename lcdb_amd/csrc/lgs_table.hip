@@ -120,34 +120,71 @@ __device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {        // crc32c.h:
 constexpr uint32_t kImgWords = kPass / 4 + kPass / 64 + 8;
 __device__ __forceinline__ uint32_t pidx(uint32_t m) { return m + (m >> 4); }
 
-// Stages the pass whose virtual byte 0 is data index lo: every V_m holding a
-// data byte of [a, b) (m < 1024).  Other dwords are left as they were.
-// Reads whole aligned 16-byte granules of the source (coalesced, one per
-// lane) plus the dword after each; never a granule without a byte of
-// src[a .. b + 16).
-__device__ __forceinline__ void stage_pass(uint32_t* img, gptr<const uint8_t> src, int64_t lo,
-                                           uint32_t a, uint32_t b) {
+// A pass's source granules in registers: this lane's granule k is the
+// aligned 16 bytes at g_lo + 16 (lane + 64 k), plus the dword after them;
+// a pass covers at most 4 096 data bytes, so 5 granules a lane reach past it.
+constexpr uint32_t kPassGr = 5;
+struct PassLoad {
+  u32x4 q[kPassGr];
+  uint32_t nx[kPassGr];
+};
+
+// Issues the loads of the pass covering data [a, b) (all of them before any
+// is used, so their latencies overlap; never a granule without a byte of
+// src[a .. b + 16)).
+__device__ __forceinline__ void load_pass(PassLoad& r, gptr<const uint8_t> src, uint32_t a,
+                                          uint32_t b) {
+  if (a >= b) return;
+  const uint64_t s0 = (uint64_t)(uintptr_t)src;
+  const uint64_t g_lo = (s0 + a) & ~15ull, g_hi = (s0 + b + 15) & ~15ull;
+#pragma unroll
+  for (uint32_t k = 0; k < kPassGr; ++k) {
+    const uint64_t g = g_lo + 16ull * (lane_id() + kWave * k);
+    if (g < g_hi) {
+      r.q[k] = *(gptr<const u32x4>)(src + (int64_t)(g - s0));
+      r.nx[k] = *(gptr<const uint32_t>)(src + (int64_t)(g + 16 - s0));
+    }
+  }
+}
+
+// Stages the pass whose virtual byte 0 is data index lo from its loads: every
+// V_m holding a data byte of [a, b) (m < 1024).  Other dwords are left as
+// they were.
+__device__ __forceinline__ void store_pass(uint32_t* img, const PassLoad& r,
+                                           gptr<const uint8_t> src, int64_t lo, uint32_t a,
+                                           uint32_t b) {
   if (a >= b) return;
   const uint64_t s0 = (uint64_t)(uintptr_t)src;
   const uint64_t sb = s0 + (uint64_t)lo;                     // address of virtual byte 0
   const uint32_t sh = (uint32_t)(sb & 3u);
   const uint64_t ab = sb - sh;                               // V_m = bytes ab + 4m + sh ..
   const uint64_t g_lo = (s0 + a) & ~15ull, g_hi = (s0 + b + 15) & ~15ull;
-  for (uint64_t g = g_lo + 16ull * lane_id(); g < g_hi; g += 16ull * kWave) {
-    const u32x4 q = *(gptr<const u32x4>)(src + (int64_t)(g - s0));
-    const uint32_t nx = *(gptr<const uint32_t>)(src + (int64_t)(g + 16 - s0));
-    const int32_t i0 = (int32_t)((int64_t)(g - ab) >> 2);    // dword index of q.x
-    const uint32_t v[5] = {__builtin_amdgcn_alignbyte(q.x, 0u, sh),   // bytes before g: never data
-                           __builtin_amdgcn_alignbyte(q.y, q.x, sh),
-                           __builtin_amdgcn_alignbyte(q.z, q.y, sh),
-                           __builtin_amdgcn_alignbyte(q.w, q.z, sh),
-                           __builtin_amdgcn_alignbyte(nx, q.w, sh)};
 #pragma unroll
-    for (int r = 0; r < 5; ++r) {
-      const int32_t m = i0 - 1 + r;
-      if ((r > 0 || g == g_lo) && m >= 0 && m < (int32_t)(kPass / 4)) img[pidx((uint32_t)m)] = v[r];
+  for (uint32_t k = 0; k < kPassGr; ++k) {
+    const uint64_t g = g_lo + 16ull * (lane_id() + kWave * k);
+    if (g < g_hi) {
+      const u32x4 q = r.q[k];
+      const uint32_t nx = r.nx[k];
+      const int32_t i0 = (int32_t)((int64_t)(g - ab) >> 2);  // dword index of q.x
+      const uint32_t v[5] = {__builtin_amdgcn_alignbyte(q.x, 0u, sh),   // bytes before g: never data
+                             __builtin_amdgcn_alignbyte(q.y, q.x, sh),
+                             __builtin_amdgcn_alignbyte(q.z, q.y, sh),
+                             __builtin_amdgcn_alignbyte(q.w, q.z, sh),
+                             __builtin_amdgcn_alignbyte(nx, q.w, sh)};
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int32_t m = i0 - 1 + t;
+        if ((t > 0 || g == g_lo) && m >= 0 && m < (int32_t)(kPass / 4)) img[pidx((uint32_t)m)] = v[t];
+      }
     }
   }
+}
+
+__device__ __forceinline__ void stage_pass(uint32_t* img, gptr<const uint8_t> src, int64_t lo,
+                                           uint32_t a, uint32_t b) {
+  PassLoad r;
+  load_pass(r, src, a, b);
+  store_pass(img, r, src, lo, a, b);
 }
 
 // Byte v (0 <= v < 4096 + 16) of a staged pass.
@@ -229,10 +266,14 @@ __device__ uint32_t wave_crc(const Crc& T, uint32_t* img, gptr<const uint8_t> sr
           c = T.dword(c, (raw & vm) ^ cm);                    // ~0 pre-conditioning
         }
       }
+      // Six levels: lane i (i a multiple of 2^(lv+1)) joins its group with
+      // the next one, c = c * x^(512 * 2^lv) ^ c(i + 2^lv).  Only those lanes
+      // do the shift's 8 table lookups (all 64 doing them was ~half of the
+      // kernel's LDS reads).
 #pragma unroll
-      for (uint32_t lv = 0; lv < 6; ++lv) {                   // lanes i, i + 2^lv
-        const uint32_t other = (uint32_t)__shfl_xor((int)c, 1 << lv);
-        c = T.shift(lv, c) ^ other;
+      for (uint32_t lv = 0; lv < 6; ++lv) {
+        const uint32_t other = (uint32_t)__shfl_down((int)c, 1u << lv);
+        if ((lane & ((2u << lv) - 1u)) == 0) c = T.shift(lv, c) ^ other;
       }
       const uint32_t pc = uni(c);                             // lane 0: the whole pass
       acc = p == 0 ? pc : uni(T.shift(6, vec(acc)) ^ pc);

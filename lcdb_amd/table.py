@@ -63,13 +63,27 @@ def crc32c_batch(d_in, d_off, d_len, d_type=None, masked: bool = True, d_crc=Non
     return d_crc
 
 
+def write_buffers(n: int, raw_total: int, device, base: int = 0):
+    """The output and scratch tensors of write_blocks, allocated once (a
+    caller framing the same shape repeatedly passes them as `bufs`)."""
+    torch = _torch()
+    nscr = int(_L.lgs_table_write_scratch(n, raw_total))
+    return (torch.empty(raw_total + LGS_TRAILER_SIZE * n + 16, dtype=torch.uint8, device=device),
+            torch.empty(n, dtype=torch.int64, device=device),
+            torch.empty(n, dtype=torch.int64, device=device),
+            torch.full((1,), base, dtype=torch.int64, device=device),
+            torch.empty(max(nscr, 1), dtype=torch.uint8, device=device))
+
+
 def write_blocks(d_raw, d_off, d_len, compression: int = LGS_SNAPPY_COMPRESSION, base: int = 0,
-                 max_len: Optional[int] = None, raw_total: Optional[int] = None, stream=None):
+                 max_len: Optional[int] = None, raw_total: Optional[int] = None, stream=None,
+                 bufs=None):
     """Frame n raw data blocks into a contiguous file region.
 
     Returns (d_file, d_handle_off, d_handle_size, d_end): d_file[j] is file
     offset base + j, d_end[0] = base + bytes written (read it after the
-    stream syncs).  d_raw must stay readable 16 bytes past every block."""
+    stream syncs).  d_raw must stay readable 16 bytes past every block.
+    bufs: write_buffers(n, raw_total, device, base), reused."""
     torch = _torch()
     n = int(d_len.numel())
     dev = d_raw.device
@@ -77,12 +91,8 @@ def write_blocks(d_raw, d_off, d_len, compression: int = LGS_SNAPPY_COMPRESSION,
         lens = d_len.to(torch.int64)
         max_len = int(lens.max()) if n else 0
         raw_total = int(lens.sum()) if n else 0
-    d_file = torch.empty(raw_total + LGS_TRAILER_SIZE * n + 16, dtype=torch.uint8, device=dev)
-    hoff = torch.empty(n, dtype=torch.int64, device=dev)
-    hsize = torch.empty(n, dtype=torch.int64, device=dev)
-    end = torch.full((1,), base, dtype=torch.int64, device=dev)
-    nscr = int(_L.lgs_table_write_scratch(n, raw_total))
-    scr = torch.empty(max(nscr, 1), dtype=torch.uint8, device=dev)
+    d_file, hoff, hsize, end, scr = bufs if bufs is not None else write_buffers(n, raw_total, dev, base)
+    nscr = int(scr.numel())
     check(_L.lgs_table_write_dev(d_raw.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n,
                                  int(max_len), int(raw_total), int(compression), int(base),
                                  d_file.data_ptr(), hoff.data_ptr(), hsize.data_ptr(),
@@ -93,9 +103,10 @@ def write_blocks(d_raw, d_off, d_len, compression: int = LGS_SNAPPY_COMPRESSION,
 
 def read_blocks(d_file, file_len: int, d_hoff, d_hsize, d_out, d_out_off, d_out_cap,
                 max_out_cap: int, verify: bool = True, d_out_len=None, d_status=None,
-                stream=None):
+                stream=None, scratch=None):
     """ldb_read_block for every handle; returns (d_out_len, d_status).
-    d_file must stay readable 16 bytes past file_len."""
+    d_file must stay readable 16 bytes past file_len.  scratch: a uint8
+    tensor of lgs_table_read_scratch(n) bytes, reused."""
     torch = _torch()
     n = int(d_hoff.numel())
     dev = d_file.device
@@ -103,8 +114,11 @@ def read_blocks(d_file, file_len: int, d_hoff, d_hsize, d_out, d_out_off, d_out_
         d_out_len = torch.zeros(n, dtype=torch.int32, device=dev)
     if d_status is None:
         d_status = torch.zeros(n, dtype=torch.uint8, device=dev)
-    nscr = int(_L.lgs_table_read_scratch(n))
-    scr = torch.empty(max(nscr, 1), dtype=torch.uint8, device=dev)
+    if scratch is None:
+        scratch = torch.empty(max(int(_L.lgs_table_read_scratch(n)), 1), dtype=torch.uint8,
+                              device=dev)
+    scr = scratch
+    nscr = int(scr.numel())
     check(_L.lgs_table_read_dev(d_file.data_ptr(), int(file_len), d_hoff.data_ptr(),
                                 d_hsize.data_ptr(), n, 1 if verify else 0, d_out.data_ptr(),
                                 d_out_off.data_ptr(), d_out_cap.data_ptr(), int(max_out_cap),

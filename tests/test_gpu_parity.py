@@ -300,13 +300,58 @@ def test_misaligned_blocks_c1_round_trip(gpu, digests, force, shift):
         assert corpus.digest_of_digests(corpus.block_digests(ho.buf, ho.off, ho.len)) == d["raw_dd"]
 
 
+def _guarded_page(hip, size):
+    """A device mapping of `size` bytes (a multiple of the VMM granularity)
+    followed by a reserved, unmapped granule: any read past the mapping
+    faults.  Returns (base, release)."""
+    import ctypes as C
+
+    class Loc(C.Structure):
+        _fields_ = [("type", C.c_int), ("id", C.c_int)]
+
+    class Flags(C.Structure):
+        _fields_ = [("compressionType", C.c_ubyte), ("gpuDirectRDMACapable", C.c_ubyte),
+                    ("usage", C.c_ushort)]
+
+    class Prop(C.Structure):
+        _fields_ = [("type", C.c_int), ("requestedHandleType", C.c_int), ("location", Loc),
+                    ("win32HandleMetaData", C.c_void_p), ("allocFlags", Flags)]
+
+    class Access(C.Structure):
+        _fields_ = [("location", Loc), ("flags", C.c_int)]
+
+    dev = C.c_int()
+    assert hip.hipGetDevice(C.byref(dev)) == 0
+    prop = Prop(type=1, requestedHandleType=0, location=Loc(1, dev.value))   # pinned, device
+    gran = C.c_size_t()
+    assert hip.hipMemGetAllocationGranularity(C.byref(gran), C.byref(prop), 0) == 0
+    g = gran.value
+    size = (size + g - 1) // g * g
+    base = C.c_void_p()
+    assert hip.hipMemAddressReserve(C.byref(base), C.c_size_t(size + g), C.c_size_t(0),
+                                    C.c_void_p(0), C.c_ulonglong(0)) == 0
+    handle = C.c_void_p()
+    assert hip.hipMemCreate(C.byref(handle), C.c_size_t(size), C.byref(prop), C.c_ulonglong(0)) == 0
+    assert hip.hipMemMap(base, C.c_size_t(size), C.c_size_t(0), handle, C.c_ulonglong(0)) == 0
+    acc = Access(location=Loc(1, dev.value), flags=3)                    # read-write
+    assert hip.hipMemSetAccess(base, C.c_size_t(size), C.byref(acc), C.c_size_t(1)) == 0
+
+    def release():
+        hip.hipMemUnmap(base, C.c_size_t(size))
+        hip.hipMemRelease(handle)
+        hip.hipMemAddressFree(base, C.c_size_t(size + g))
+
+    return base.value, size, release
+
+
 def test_encode_block_flush_with_allocation_end(gpu):
-    # lgs_encode_batch_dev promises no read slack, so a block whose
-    # last byte is the last byte of its device allocation must be encoded
+    # ADVICE r3/r4: lgs_encode_batch_dev promises no read slack, so a block
+    # whose last byte is the last byte of its device memory must be encoded
     # from inside it (the staging reads a ragged last granule as the 16 bytes
     # ending at the block's end, and a block under 16 bytes a byte per lane).
-    # Every length residue mod 16, each block alone at the end of its own
-    # page-multiple hipMalloc, against the reference encoder.
+    # Every length residue mod 16, each block flush with the end of a VMM
+    # mapping whose next granule is reserved and unmapped (an overread faults
+    # instead of reading a neighbour), against the reference encoder.
     import ctypes as C
     import torch
     from lcdb_amd import _native
@@ -317,14 +362,16 @@ def test_encode_block_flush_with_allocation_end(gpu):
     fill = corpus.fillseq(20)
     lengths = list(range(1, 49)) + [4096 + k for k in range(-16, 17)] + \
         [16384 + 9, 65536 - 5, 65536, 65536 + 7, 70001]
-    for L in lengths:
-        raw = bytes(fill.buf[:L]) if L <= len(fill.buf) else bytes(rng.integers(0, 4, L, dtype=np.uint8))
-        size = (L + 4095) // 4096 * 4096
-        p = C.c_void_p()
-        assert hip.hipMalloc(C.byref(p), C.c_size_t(size)) == 0
-        try:
+    base, size, release = _guarded_page(hip, 70001 + 16)
+    try:
+        # (The granule after the mapping is reserved and never mapped, by
+        # construction; hipPointerGetAttributes reports reserved-unmapped
+        # addresses as valid, so it cannot witness that.)
+        for L in lengths:
+            raw = bytes(fill.buf[:L]) if L <= len(fill.buf) else \
+                bytes(rng.integers(0, 4, L, dtype=np.uint8))
             src = np.frombuffer(raw, dtype=np.uint8)
-            assert hip.hipMemcpy(C.c_void_p(p.value + size - L), C.c_void_p(src.ctypes.data),
+            assert hip.hipMemcpy(C.c_void_p(base + size - L), C.c_void_p(src.ctypes.data),
                                  C.c_size_t(L), 1) == 0
             off = torch.tensor([size - L], dtype=torch.int64, device="cuda")
             ln = torch.tensor([L], dtype=torch.int32, device="cuda")
@@ -332,16 +379,16 @@ def test_encode_block_flush_with_allocation_end(gpu):
             ooff = torch.zeros(1, dtype=torch.int64, device="cuda")
             olen = torch.zeros(1, dtype=torch.int32, device="cuda")
             s = torch.cuda.current_stream()
-            _native.check(lib.lgs_encode_batch_dev(p.value, off.data_ptr(), ln.data_ptr(),
+            _native.check(lib.lgs_encode_batch_dev(C.c_void_p(base), off.data_ptr(), ln.data_ptr(),
                                                    out.data_ptr(), ooff.data_ptr(),
                                                    olen.data_ptr(), 1, L, s.cuda_stream),
                           "lgs_encode_batch_dev")
             s.synchronize()
             got = out[:int(olen.item())].cpu().numpy().tobytes()
             assert got == ref.encode(raw), L
-        finally:
-            torch.cuda.synchronize()
-            hip.hipFree(p)
+    finally:
+        torch.cuda.synchronize()
+        release()
 
 
 def test_encode_c2_and_random(gpu, digests):

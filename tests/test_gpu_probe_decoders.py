@@ -22,15 +22,37 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+# Every probe case test_gpu_parity.py defines (its parametrizations over the
+# quad, ops, group, chain, trips decoders): the child must pass exactly these,
+# so a case that silently stops being collected fails here.
+EXPECTED = {
+    "test_decode_kernel_variants_golden[quad]", "test_decode_kernel_variants_golden[ops]",
+    "test_decode_kernel_variants_golden[group]", "test_decode_kernel_variants_golden[chain]",
+    "test_decode_kernels_c2_full_size[kernels1]",
+    "test_decode_ring_c3_mixed_and_odd_slots[quad]", "test_decode_ring_c3_mixed_and_odd_slots[ops]",
+    "test_decode_ring_c3_mixed_and_odd_slots[group]",
+    "test_decode_ops_rejects_overflow_and_jumps",
+    "test_decode_in_place_runahead[quad]", "test_decode_in_place_runahead[ops]",
+    "test_decode_in_place_runahead[group]", "test_decode_in_place_runahead[chain]",
+    "test_decode_wide_far_copies_long_literals_and_rejects[trips]",
+    "test_decode_wide_dependent_copies_and_c3[trips]",
+    "test_decode_wide_dependent_copies_and_c3[group]",
+    "test_decode_small_batch_kernels_and_rejects[group-4608]",
+    "test_decode_small_batch_kernels_and_rejects[group-16896]",
+    "test_decode_small_batch_kernels_and_rejects[group-66048]",
+    "test_decode_small_batch_kernels_and_rejects[chain-4608]",
+    "test_decode_small_batch_kernels_and_rejects[chain-16896]",
+}
+
+
 def test_probe_decoders_parity():
     env = dict(os.environ, LGS_TEST_PROBE="1")
-    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-q", "-p", "no:cacheprovider",
+    r = subprocess.run([sys.executable, "-u", "-m", "pytest", "-v", "-p", "no:cacheprovider",
                         "-m", "gpu and probe", "--timeout", "300", "--timeout-method", "thread",
                         os.path.join(ROOT, "tests", "test_gpu_parity.py")],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=1100)
     tail = (r.stdout + r.stderr)[-4000:]
     assert r.returncode == 0, tail
-    m = re.search(r"(\d+) passed", r.stdout)
-    # quad and ops: golden, C2 (one test), C3, runahead; ops rejects; trips: two wide
-    assert m and int(m.group(1)) >= 10, tail
+    passed = set(re.findall(r"test_gpu_parity\.py::(\S+) PASSED", r.stdout))
+    assert passed == EXPECTED, (sorted(EXPECTED - passed), sorted(passed - EXPECTED), tail)
     assert not re.search(r"\d+ (skipped|failed|error)", r.stdout), tail
