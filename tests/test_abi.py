@@ -138,3 +138,15 @@ def test_product_has_only_the_kept_decoders():
     probe = open(build.PROBE_LIB, "rb").read()
     assert b"decode_quad_kernel" in probe and b"op_exec_kernel" in probe
     assert b"decode_group_kernel" in probe and b"decode_chain_kernel" in probe
+
+
+def test_service_option_and_kernels():
+    """The drop-in service: its two resident kernels are in the
+    product, and lgs_set_option("service", ...) takes 0 or 1 only (no GPU)."""
+    blob = open(build.LIB, "rb").read()
+    assert b"encode_service_kernel" in blob and b"decode_service_kernel" in blob
+    lib = _native.lib()
+    for v in ("2", "", "on"):
+        assert lib.lgs_set_option(b"service", v.encode()) == _native.LGS_EINVAL, v
+    for v in ("0", "1"):
+        assert lib.lgs_set_option(b"service", v.encode()) == _native.LGS_OK, v

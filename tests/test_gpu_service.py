@@ -63,11 +63,6 @@ def test_service_equals_reference_and_launch_path(gpu, vectors, force):
             assert dec == want_dec, mode
 
 
-def test_service_rejects_bad_option():
-    with pytest.raises(Exception):
-        _native.set_option("service", "2")
-
-
 _CHILD = textwrap.dedent("""
     import sys, time
     sys.path.insert(0, {root!r})
