@@ -884,7 +884,6 @@ __global__ __launch_bounds__(64) void decode_ring_kernel(
   // active lane (every block's header corrupt) does nothing.
   LGS_RING_TRIPS_DECL;
   LGS_RING_PH_DECL;
-  LGS_RING_START();
   do {
     LGS_RING_TRIP();
     LGS_RING_PH_TRIP();

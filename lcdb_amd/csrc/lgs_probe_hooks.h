@@ -141,16 +141,3 @@ __device__ __forceinline__ uint32_t lgs_ring_ph_value_(const uint32_t* ph, uint3
 #define LGS_ENC_PH_STAGED() do {} while (0)
 #define LGS_ENC_PH_END(SLOT, LEN) do {} while (0)
 #endif
-
-// ---- decode_ring_kernel wave start (A/B of co-resident waves' phase) -------
-// LGS_PROBE_RING_STAGGER=N: waves of odd workgroups sleep N x 64 cycles before
-// their first trip; LGS_PROBE_RING_PRIO: they run at s_setprio 1.
-#if defined(LGS_PROBE_RING_STAGGER)
-#define LGS_RING_START()                                                   \
-  do { if (blockIdx.x & 1u) { for (int s_ = 0; s_ < LGS_PROBE_RING_STAGGER / 127; ++s_) \
-         __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(LGS_PROBE_RING_STAGGER % 127); } } while (0)
-#elif defined(LGS_PROBE_RING_PRIO)
-#define LGS_RING_START() do { if (blockIdx.x & 1u) __builtin_amdgcn_s_setprio(1); } while (0)
-#else
-#define LGS_RING_START() do {} while (0)
-#endif
