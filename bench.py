@@ -307,12 +307,16 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
                      "ms_per_step": tp / a.steps * 1e3,
                      "note": "encode(step k) || decode(step k-1) on two streams; extra field, "
                              "not value"}
-        # The same on disjoint CU sets (hipExtStreamCreateWithCUMask), sized by
-        # the two kernels' C2 times (~2:1): each kernel keeps its own LDS
-        # occupancy instead of the two thrashing each other's.
-        cu = cu_partition_streams(dev_index)
+        # The same on disjoint CU sets (hipExtStreamCreateWithCUMask): each
+        # kernel keeps its own LDS occupancy instead of the two thrashing each
+        # other's.  Workgroups go round-robin to the XCDs, so every XCD gets the
+        # same decode share (cu_partition_streams); the share is the one whose
+        # slower kernel, each timed alone on its CUs, is fastest (untimed).
+        cu = choose_cu_partition(
+            dev_index, lambda s: batch.encode(raws[0], comps[0], s),
+            lambda s: batch.decode(comps[0], outs[0], stats[0], s))
         if cu is not None:
-            s_enc, s_dec, split = cu
+            s_enc, s_dec, split, alone = cu
             batch.encode(raws[0], comps[0], s_enc)
             enc_done[0].record(s_enc)
             torch.cuda.synchronize()
@@ -333,8 +337,9 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
             pipelined["cu_partition"] = {
                 "GiBps": raw_bytes * world * a.steps / tp / 2**30,
                 "ms_per_step": tp / a.steps * 1e3, "cus_encode_decode": split,
-                "note": "encode and decode streams on disjoint CU sets (CU i -> decode when "
-                        "i % 3 == 2)"}
+                "alone_us_encode_decode": alone,
+                "note": "encode and decode streams on disjoint CU sets (the same decode CUs "
+                        "in every XCD), the split whose slower kernel alone is fastest"}
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
@@ -521,11 +526,60 @@ def corpus_digests(c):
     return corpus.block_digests(c.buf, c.off, c.len)
 
 
-def cu_partition_streams(dev_index: int):
-    """Two HIP streams on disjoint CUs of this GPU: encode gets CUs i with
-    i % 3 != 2, decode the rest (the kernels' C2 times are ~2:1).  Returns
+N_XCD = 8        # MI355X: 8 XCDs of 32 CUs
+
+
+def choose_cu_partition(dev_index: int, enc_fn, dec_fn, shares=range(8, 17)):
+    """The decode share (CUs per XCD) whose slower kernel, each timed alone
+    on its CU set with HIP events (best of 2 after a warm-up), is fastest.
+    Returns (encode stream, decode stream, [n_encode_cus, n_decode_cus],
+    [encode_us, decode_us]) or None where masks are refused.  The streams of
+    the other shares are destroyed."""
+    import ctypes as C
+    import torch
+    hip = C.CDLL("libamdhip64.so")
+
+    def alone(fn, s):
+        ts = []
+        for k in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            fn(s)
+            e1.record(s)
+            e1.synchronize()
+            if k:
+                ts.append(e0.elapsed_time(e1) * 1e3)
+        return min(ts)
+
+    best = None
+    for nx in shares:
+        cu = cu_partition_streams(dev_index, nx)
+        if cu is None:
+            return None
+        s_enc, s_dec, split = cu
+        t = [round(alone(enc_fn, s_enc), 1), round(alone(dec_fn, s_dec), 1)]
+        if best is None or max(t) < max(best[3]):
+            if best is not None:
+                hip.hipStreamDestroy(C.c_void_p(best[0].cuda_stream))
+                hip.hipStreamDestroy(C.c_void_p(best[1].cuda_stream))
+            best = (s_enc, s_dec, split, t)
+        else:
+            hip.hipStreamDestroy(C.c_void_p(s_enc.cuda_stream))
+            hip.hipStreamDestroy(C.c_void_p(s_dec.cuda_stream))
+    return best
+
+
+def cu_partition_streams(dev_index: int, dec_per_xcd: int):
+    """Two HIP streams on disjoint CUs of this GPU: dec_per_xcd CUs of every
+    XCD for the decode stream, the rest for the encode stream.  Returns
     (encode stream, decode stream, [n_encode_cus, n_decode_cus]) as torch
-    ExternalStreams, or None where the runtime refuses the mask."""
+    ExternalStreams, or None where the runtime refuses the mask.
+
+    Mask bit i belongs to XCD i % N_XCD (measured, tools/cu_mask_map.py,
+    profiles/r5y_cu_mask_map.json: bits [0, 8k) run a kernel on about 8k
+    CUs, while one bit in eight -- all of one XCD -- runs it on the whole
+    chip: an XCD left without a bit is not masked at all).  So the decode
+    share is the contiguous bits [0, N_XCD * dec_per_xcd)."""
     import ctypes as C
     import torch
     try:
@@ -536,7 +590,7 @@ def cu_partition_streams(dev_index: int):
     words = (ncu + 31) // 32
     enc, dec = [0] * words, [0] * words
     for i in range(ncu):
-        (dec if i % 3 == 2 else enc)[i // 32] |= 1 << (i % 32)
+        (dec if i < N_XCD * dec_per_xcd else enc)[i // 32] |= 1 << (i % 32)
     out = []
     for m in (enc, dec):
         s = C.c_void_p()
