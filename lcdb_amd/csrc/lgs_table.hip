@@ -18,15 +18,19 @@
 //    change the unconditioned CRC (register 0 stays 0), and the ~0
 //    pre-conditioning equals complementing the message's first 4 bytes, so
 //    every pass is 64 equal segments and every lane does identical work;
+//  * a lane loads the aligned 16-byte granules under its segment (only
+//    granules holding a byte of the block: never another page) and shifts
+//    them into place in registers by the pass's misalignment, which is the
+//    same for every lane (no LDS image);
 //  * a lane folds its 16 dwords with slice-by-4 tables (4 LDS lookups per
-//    dword);
-//  * six butterfly levels (ds_bpermute) combine lane pairs: shift the left
-//    CRC by 64 * 2^k zero bytes (multiply by x^(512 * 2^k) mod P, eight
-//    nibble-table lookups) and xor the right one; passes combine the same
-//    way with the 4096-byte shift.
-// The block is staged pass by pass in LDS with 16-byte aligned loads; the
-// same LDS image feeds the copy to the destination (the file image on the
-// write path, the output slot of a raw block on the read path).
+//    dword), then multiplies its CRC by x^(512 (63 - lane)) -- the zero
+//    bytes after its segment -- with a table of its own (eight nibble
+//    lookups), and one xor-reduction over the wave (DPP) gives the pass's
+//    CRC.  The CRC of the passes before enters as lane 0's start register.
+// A lane's registers also feed the copy to the destination (the file image
+// on the write path, the output slot of a raw block on the read path): its
+// whole 16-byte chunks are stored as they are, the first 16 bytes of the
+// block (and, without its type byte, the last 16) by one lane each.
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
@@ -38,8 +42,9 @@ constexpr uint32_t kMaskDelta = 0xa282ead8u;  // crc32c.h:38
 constexpr uint32_t kTrailer = 5;              // type byte + fixed32 crc (format.h)
 constexpr uint32_t kSeg = 64;                 // bytes per lane per pass
 constexpr uint32_t kPass = kSeg * kWave;      // 4096
-constexpr uint32_t kLevels = 7;               // shifts by 64 * 2^k bytes, k = 0..6
-constexpr uint32_t kTabWords = 4 * 256 + kLevels * 128;
+constexpr uint32_t kLaneBase = 1024;          // after the slice-by-4 tables
+constexpr uint32_t kLaneStride = 129;         // 128 words a lane, +1 spreads the banks
+constexpr uint32_t kTabWords = kLaneBase + kLaneStride * kWave;
 
 // a * b mod P over GF(2), reflected (bit 31 is x^0).
 constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
@@ -54,7 +59,8 @@ constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
 struct CrcTables {
   uint32_t w[kTabWords];
   // w[k*256 + b]          slice-by-4: byte b followed by k zero bytes
-  // w[1024 + k*128 + 16j + v]  v << 4j times x^(512 * 2^k)
+  // w[1024 + 129*L + 16j + v]  (v << 4j) times x^(512 * (63 - L)): lane L's
+  //                        segment followed by the 63 - L segments after it
   constexpr CrcTables() : w() {
     for (uint32_t b = 0; b < 256; ++b) {
       uint32_t c = b;
@@ -66,12 +72,23 @@ struct CrcTables {
         const uint32_t prev = w[(k - 1) * 256 + b];
         w[k * 256 + b] = (prev >> 8) ^ w[prev & 0xffu];
       }
-    uint32_t xp = 0x40000000u;                       // x^1
-    for (int j = 0; j < 9; ++j) xp = gf_mul(xp, xp); // x^512: 64 zero bytes
-    for (uint32_t k = 0; k < kLevels; ++k) {
-      for (uint32_t j = 0; j < 8; ++j)
-        for (uint32_t v = 0; v < 16; ++v) w[1024 + k * 128 + 16 * j + v] = gf_mul(xp, v << (4 * j));
-      xp = gf_mul(xp, xp);
+    uint32_t x512 = 0x40000000u;                         // x^1
+    for (int j = 0; j < 9; ++j) x512 = gf_mul(x512, x512); // x^512: 64 zero bytes
+    uint32_t xp = 0x80000000u;                           // x^0 for lane 63
+    for (int L = (int)kWave - 1; L >= 0; --L) {
+      uint32_t bx[32] = {};                              // bx[i] = xp * x^i
+      bx[0] = xp;
+      for (int i = 1; i < 32; ++i) bx[i] = (bx[i - 1] & 1u) ? (bx[i - 1] >> 1) ^ kPoly : (bx[i - 1] >> 1);
+      for (uint32_t j = 0; j < 8; ++j) {
+        uint32_t* t = w + kLaneBase + kLaneStride * (uint32_t)L + 16 * j;
+        t[0] = 0;
+        for (uint32_t v = 1; v < 16; ++v) {
+          uint32_t b = 0;
+          while (!((v >> b) & 1u)) ++b;
+          t[v] = t[v & (v - 1)] ^ bx[31 - (4 * j + b)];  // bit 4j+b is x^(31-4j-b)
+        }
+      }
+      xp = gf_mul(xp, x512);
     }
   }
 };
@@ -90,9 +107,9 @@ struct Crc {
   __device__ __forceinline__ uint32_t byte(uint32_t crc, uint32_t b) const {
     return w[(crc ^ b) & 255u] ^ (crc >> 8);
   }
-  // crc followed by 64 * 2^k zero bytes.
-  __device__ __forceinline__ uint32_t shift(uint32_t k, uint32_t a) const {
-    const uint32_t* n = w + 1024 + k * 128;
+  // crc followed by 64 * (63 - lane) zero bytes.
+  __device__ __forceinline__ uint32_t lane_shift(uint32_t a, uint32_t lane) const {
+    const uint32_t* n = w + kLaneBase + kLaneStride * lane;
     uint32_t r = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) r ^= n[16 * j + ((a >> (4 * j)) & 15u)];
@@ -113,173 +130,139 @@ __device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {        // crc32c.h:
   return (r >> 17) | (r << 15);
 }
 
-// One pass staged in LDS as its 1024 virtual dwords V_m (bytes 4m .. 4m+3
-// of the pass), re-aligned to the pass's byte 0 and stored at dword index
-// m + m / 16: lane L's segment (V_16L .. V_16L+15) starts at dword 17 L, so
-// the 64 lanes reading dword j of their segments hit 64 different banks.
-constexpr uint32_t kImgWords = kPass / 4 + kPass / 64 + 8;
-__device__ __forceinline__ uint32_t pidx(uint32_t m) { return m + (m >> 4); }
+// Xor of v over the wave: a prefix within each row of 16 lanes (DPP
+// row_shr 1, 2, 4, 8; lanes shifted in from outside the row read 0), then
+// the four rows' last lanes.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  return lane_val(v, 15) ^ lane_val(v, 31) ^ lane_val(v, 47) ^ lane_val(v, 63);
+}
 
-// A pass's source granules in registers: this lane's granule k is the
-// aligned 16 bytes at g_lo + 16 (lane + 64 k), plus the dword after them;
-// a pass covers at most 4 096 data bytes, so 5 granules a lane reach past it.
-constexpr uint32_t kPassGr = 5;
-struct PassLoad {
-  u32x4 q[kPassGr];
-  uint32_t nx[kPassGr];
-};
+typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 
-// Issues the loads of the pass covering data [a, b) (all of them before any
-// is used, so their latencies overlap; never a granule without a byte of
-// src[a .. b + 16)).
-__device__ __forceinline__ void load_pass(PassLoad& r, gptr<const uint8_t> src, uint32_t a,
-                                          uint32_t b) {
-  if (a >= b) return;
-  const uint64_t s0 = (uint64_t)(uintptr_t)src;
-  const uint64_t g_lo = (s0 + a) & ~15ull, g_hi = (s0 + b + 15) & ~15ull;
+// Dword i of this lane's segment is bytes sh + 4i .. sh + 4i + 3 of its
+// five granules g (sh = 4Q + (sh & 3), Q uniform).
+template <uint32_t Q>
+__device__ __forceinline__ void funnel(const u32x4 (&g)[5], uint32_t r, uint32_t (&v)[16]) {
+  uint32_t W[20];
 #pragma unroll
-  for (uint32_t k = 0; k < kPassGr; ++k) {
-    const uint64_t g = g_lo + 16ull * (lane_id() + kWave * k);
-    if (g < g_hi) {
-      r.q[k] = *(gptr<const u32x4>)(src + (int64_t)(g - s0));
-      r.nx[k] = *(gptr<const uint32_t>)(src + (int64_t)(g + 16 - s0));
-    }
+  for (uint32_t t = 0; t < 5; ++t) {
+    W[4 * t] = g[t].x;
+    W[4 * t + 1] = g[t].y;
+    W[4 * t + 2] = g[t].z;
+    W[4 * t + 3] = g[t].w;
   }
-}
-
-// Stages the pass whose virtual byte 0 is data index lo from its loads: every
-// V_m holding a data byte of [a, b) (m < 1024).  Other dwords are left as
-// they were.
-__device__ __forceinline__ void store_pass(uint32_t* img, const PassLoad& r,
-                                           gptr<const uint8_t> src, int64_t lo, uint32_t a,
-                                           uint32_t b) {
-  if (a >= b) return;
-  const uint64_t s0 = (uint64_t)(uintptr_t)src;
-  const uint64_t sb = s0 + (uint64_t)lo;                     // address of virtual byte 0
-  const uint32_t sh = (uint32_t)(sb & 3u);
-  const uint64_t ab = sb - sh;                               // V_m = bytes ab + 4m + sh ..
-  const uint64_t g_lo = (s0 + a) & ~15ull, g_hi = (s0 + b + 15) & ~15ull;
 #pragma unroll
-  for (uint32_t k = 0; k < kPassGr; ++k) {
-    const uint64_t g = g_lo + 16ull * (lane_id() + kWave * k);
-    if (g < g_hi) {
-      const u32x4 q = r.q[k];
-      const uint32_t nx = r.nx[k];
-      const int32_t i0 = (int32_t)((int64_t)(g - ab) >> 2);  // dword index of q.x
-      const uint32_t v[5] = {__builtin_amdgcn_alignbyte(q.x, 0u, sh),   // bytes before g: never data
-                             __builtin_amdgcn_alignbyte(q.y, q.x, sh),
-                             __builtin_amdgcn_alignbyte(q.z, q.y, sh),
-                             __builtin_amdgcn_alignbyte(q.w, q.z, sh),
-                             __builtin_amdgcn_alignbyte(nx, q.w, sh)};
-#pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const int32_t m = i0 - 1 + t;
-        if ((t > 0 || g == g_lo) && m >= 0 && m < (int32_t)(kPass / 4)) img[pidx((uint32_t)m)] = v[t];
-      }
-    }
-  }
+  for (uint32_t i = 0; i < 16; ++i) v[i] = __builtin_amdgcn_alignbyte(W[Q + i + 1], W[Q + i], r);
 }
 
-__device__ __forceinline__ void stage_pass(uint32_t* img, gptr<const uint8_t> src, int64_t lo,
-                                           uint32_t a, uint32_t b) {
-  PassLoad r;
-  load_pass(r, src, a, b);
-  store_pass(img, r, src, lo, a, b);
-}
-
-// Byte v (0 <= v < 4096 + 16) of a staged pass.
-__device__ __forceinline__ uint32_t img_byte(const uint32_t* img, uint32_t v) {
-  return (img[pidx(v >> 2)] >> (8 * (v & 3u))) & 0xffu;
-}
-
-// Writes data indices [a, e) of the staged pass (virtual byte 0 = data index
-// lo) to dst + k, any alignment: whole 16-byte destination granules with one
-// 16-byte store, the ragged granules at either end byte by byte.
-__device__ __forceinline__ void copy_out(const uint32_t* img, int64_t lo, gptr<uint8_t> dst,
-                                         uint32_t a, uint32_t e) {
-  if (a >= e) return;
-  const uint64_t d0 = (uint64_t)(uintptr_t)dst;
-  const uint64_t g_lo = (d0 + a) & ~15ull, g_hi = (d0 + e + 15) & ~15ull;
-  for (uint64_t g = g_lo + 16ull * lane_id(); g < g_hi; g += 16ull * kWave) {
-    const int64_t k0 = (int64_t)(g - d0);                    // data index of the granule
-    if (g >= d0 + a && g + 16 <= d0 + e) {
-      const uint32_t v0 = (uint32_t)(k0 - lo), m0 = v0 >> 2, t = v0 & 3u;
-      const uint32_t w0 = img[pidx(m0)], w1 = img[pidx(m0 + 1)], w2 = img[pidx(m0 + 2)],
-                     w3 = img[pidx(m0 + 3)], w4 = img[pidx(m0 + 4)];
-      const u32x4 v{__builtin_amdgcn_alignbyte(w1, w0, t), __builtin_amdgcn_alignbyte(w2, w1, t),
-                    __builtin_amdgcn_alignbyte(w3, w2, t), __builtin_amdgcn_alignbyte(w4, w3, t)};
-      *(gptr<u32x4>)(dst + k0) = v;
-    } else {
-      for (uint32_t t = 0; t < 16; ++t) {
-        const int64_t k = k0 + t;
-        if (k >= (int64_t)a && k < (int64_t)e) dst[k] = (uint8_t)img_byte(img, (uint32_t)(k - lo));
-      }
-    }
-  }
+// src[0 .. e) to dst, 16 bytes a lane per step, the ragged end as the 16
+// bytes that end at e (e >= 16; reads stay inside src[0 .. e)).
+__device__ __forceinline__ void copy_bytes(gptr<const uint8_t> src, gptr<uint8_t> dst, uint32_t e) {
+  for (uint32_t k = 16 * lane_id(); k + 16 <= e; k += 16 * kWave)
+    *(gptr<u32x4_a1>)(dst + k) = *(gptr<const u32x4_a1>)(src + k);
+  if (lane_id() == 0 && (e & 15u))
+    *(gptr<u32x4_a1>)(dst + (e - 16)) = *(gptr<const u32x4_a1>)(src + (e - 16));
 }
 
 // Conditioned CRC32C (crc32c.c:643-750) of src[0 .. len) followed by the
 // byte `type` when has_type -- the trailer CRC of table_builder.c:139-140
 // before masking.  When `copy`, src[0 .. len) is also written to dst, and
 // the type byte after it when copy_type.  want_crc == false: copy only.
-// Uniform result.  Reads may touch the 16 bytes after src[len - 1].
-__device__ uint32_t wave_crc(const Crc& T, uint32_t* img, gptr<const uint8_t> src, uint32_t len,
+// Uniform result.  Reads only the aligned 16-byte granules holding a byte of
+// src[0 .. len).
+__device__ uint32_t wave_crc(const Crc& T, gptr<const uint8_t> src, uint32_t len,
                              uint32_t has_type, uint32_t type, gptr<uint8_t> dst, bool copy,
                              bool copy_type, bool want_crc) {
   const uint32_t lane = lane_id();
   const uint32_t total = len + has_type;                      // message length L'
+  const uint32_t e = len + (copy_type ? has_type : 0u);       // bytes copied
+  const bool short_copy = e <= kWave;
+  if (copy && short_copy) {                                   // a byte a lane
+    if (lane < e) dst[lane] = lane < len ? src[lane] : (uint8_t)type;
+  }
+  if (!want_crc) {
+    if (copy && !short_copy) copy_bytes(src, dst, len);       // (copy_type unused here)
+    return 0;
+  }
   if (total < 4) {                                            // tiny: one byte at a time
     uint32_t c = ~0u;
     for (uint32_t k = 0; k < len; ++k) c = T.byte(c, src[k]);
     if (has_type) c = T.byte(c, type);
-    const uint32_t ncopy = len + (copy_type ? has_type : 0u);
-    if (copy && lane < ncopy) dst[lane] = lane < len ? src[lane] : (uint8_t)type;
     return ~c;
+  }
+  const bool chunks = copy && !short_copy;
+  if (chunks) {                                               // e > 64 >= 16: len >= 16
+    if (lane == 0) *(gptr<u32x4_a1>)dst = *(gptr<const u32x4_a1>)src;
+    if (lane == 1 && e != total)                              // the type byte not copied
+      *(gptr<u32x4_a1>)(dst + (len - 16)) = *(gptr<const u32x4_a1>)(src + (len - 16));
   }
   const uint32_t passes = (total + kPass - 1) / kPass;
   const uint32_t pad = passes * kPass - total;                // leading virtual zeros
-  uint32_t acc = 0;
+  const uint64_t s0 = (uint64_t)(uintptr_t)src;
+  uint32_t acc = 0, carry = 0;
   for (uint32_t p = 0; p < passes; ++p) {
     const int64_t lo = (int64_t)p * kPass - pad;              // data index of virtual byte 0
-    const uint32_t a = lo < 0 ? 0u : (uint32_t)lo;
-    const uint32_t b = (uint32_t)(lo + kPass < (int64_t)len ? lo + kPass : (int64_t)len);
-    const bool last = p + 1 == passes;
-    stage_pass(img, src, lo, a, b);
-    order();
-    if (last && has_type && lane == 0) {                      // virtual byte 4095
-      reinterpret_cast<uint8_t*>(img)[4 * pidx(kPass / 4 - 1) + 3] = (uint8_t)type;
+    const int64_t k0 = lo + (int64_t)(kSeg * lane);           // data index of the segment
+    const uint64_t B = s0 + (uint64_t)lo;
+    const uint32_t sh = uni((uint32_t)B & 15u);
+    const uint64_t gb = (B & ~15ull) + (uint64_t)(kSeg * lane);
+    u32x4 g[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; ++i) {
+      const uint64_t a = gb + 16ull * i;
+      g[i] = u32x4{0, 0, 0, 0};
+      if (a + 16 > s0 && a < s0 + len) g[i] = *(gptr<const u32x4>)(src + (int64_t)(a - s0));
     }
-    order();
-    if (want_crc) {
-      uint32_t c = 0;
-      const int64_t k0 = lo + (int64_t)(kSeg * lane);         // data index of the segment
-      if (k0 + (int64_t)kSeg > 0) {                           // lanes wholly in the padding skip
-#pragma unroll 4
-        for (uint32_t j = 0; j < kSeg / 4; ++j) {
-          const int32_t k = (int32_t)(k0 + 4 * j);            // data index of the dword
-          const uint32_t raw = img[17 * lane + j];
-          const uint32_t nk = (uint32_t)(-k);
-          const uint32_t part = ~0u << (8 * (nk & 3u));       // used for -4 < k < 0
-          const uint32_t vm = k >= 0 ? ~0u : (k <= -4 ? 0u : part);
-          const uint32_t head = ~0u >> (8 * ((uint32_t)k & 3u)); // used for 0 <= k < 4
-          const uint32_t cm = (k >= 4 || k <= -4) ? 0u : (k >= 0 ? head : part);
-          c = T.dword(c, (raw & vm) ^ cm);                    // ~0 pre-conditioning
+    uint32_t v[16];
+    switch (sh >> 2) {
+      case 0: funnel<0>(g, sh & 3u, v); break;
+      case 1: funnel<1>(g, sh & 3u, v); break;
+      case 2: funnel<2>(g, sh & 3u, v); break;
+      default: funnel<3>(g, sh & 3u, v); break;
+    }
+    const bool last = p + 1 == passes;
+    if (last && has_type && lane == kWave - 1) v[15] = (v[15] & 0x00ffffffu) | (type << 24);
+    if (chunks) {
+#pragma unroll
+      for (uint32_t c = 0; c < 4; ++c) {
+        const int64_t k = k0 + 16 * c;
+        if (k >= 0 && k + 16 <= (int64_t)e)
+          *(gptr<u32x4_a1>)(dst + k) = u32x4{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+      }
+    }
+    uint32_t lane_h = 0;
+    if (p == 0) {
+      // Lane lane_h holds data index 0 at segment byte zpos: zero what is
+      // before it (bytes of the granule before src) and complement data
+      // bytes 0..3 (the ~0 pre-conditioning), spilling into the next lane.
+      lane_h = pad >> 6;
+      const uint32_t zpos = pad & 63u, D = zpos >> 2, r = zpos & 3u;
+      const uint32_t hi_keep = ~0u << (8 * r), lo_spill = r ? ~0u >> (32 - 8 * r) : 0u;
+      if (lane == lane_h) {
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) {
+          const uint32_t ma = i < D ? 0u : (i == D ? hi_keep : ~0u);
+          const uint32_t mx = i == D ? hi_keep : (i == D + 1 ? lo_spill : 0u);
+          v[i] = (v[i] & ma) ^ mx;
         }
       }
-      // Six levels: lane i (i a multiple of 2^(lv+1)) joins its group with
-      // the next one, c = c * x^(512 * 2^lv) ^ c(i + 2^lv).  Only those lanes
-      // do the shift's 8 table lookups (all 64 doing them was ~half of the
-      // kernel's LDS reads).
-#pragma unroll
-      for (uint32_t lv = 0; lv < 6; ++lv) {
-        const uint32_t other = (uint32_t)__shfl_down((int)c, 1u << lv);
-        if ((lane & ((2u << lv) - 1u)) == 0) c = T.shift(lv, c) ^ other;
-      }
-      const uint32_t pc = uni(c);                             // lane 0: the whole pass
-      acc = p == 0 ? pc : uni(T.shift(6, vec(acc)) ^ pc);
+      if (D == 15 && lane == lane_h + 1) v[0] ^= lo_spill;
+      if (D == 15 && lane_h == kWave - 1) carry = lo_spill;   // into the next pass
+    } else if (p == 1) {
+      if (lane == 0) v[0] ^= carry;
     }
-    if (copy) copy_out(img, lo, dst, a, last && copy_type ? b + has_type : b);
-    order();
+    uint32_t c = 0;
+    if (lane >= lane_h) {                                     // lanes before: all padding
+      c = lane == 0 ? acc : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < 16; ++i) c = T.dword(c, v[i]);
+      c = T.lane_shift(c, lane);
+    }
+    acc = wave_xor(c);
   }
   return ~acc;
 }
@@ -292,14 +275,13 @@ __global__ __launch_bounds__(64 * WAVES) void crc_kernel(
     const uint32_t* __restrict__ in_len, const uint8_t* __restrict__ type,
     uint32_t masked, uint32_t* __restrict__ crc_out, uint32_t n) {
   __shared__ uint32_t s_tab[kTabWords];
-  __shared__ __attribute__((aligned(16))) uint32_t s_img[WAVES][kImgWords];
   load_tables(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
     const uint32_t len = uni(in_len[i]);
     const uint32_t ty = type ? uni(type[i]) : 0u;
-    const uint32_t c = wave_crc(T, s_img[wv], to_global(in) + uni64(in_off[i]), len,
+    const uint32_t c = wave_crc(T, to_global(in) + uni64(in_off[i]), len,
                                 type ? 1u : 0u, ty, nullptr, false, false, true);
     if (lane_id() == 0) crc_out[i] = masked ? crc_mask(c) : c;
   }
@@ -408,7 +390,6 @@ __global__ __launch_bounds__(64 * WAVES) void frame_kernel(
     uint8_t* __restrict__ file, uint64_t base, const uint64_t* __restrict__ foff,
     uint64_t* __restrict__ handle_off, uint64_t* __restrict__ handle_size, uint32_t n) {
   __shared__ uint32_t s_tab[kTabWords];
-  __shared__ __attribute__((aligned(16))) uint32_t s_img[WAVES][kImgWords];
   load_tables(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
@@ -421,7 +402,7 @@ __global__ __launch_bounds__(64 * WAVES) void frame_kernel(
                                          : to_global(raw) + uni64(raw_off[i]);
     const uint64_t at = uni64(foff[i]);
     const gptr<uint8_t> dst = to_global(file) + (at - base);
-    const uint32_t c = wave_crc(T, s_img[wv], src, size, 1u, comp ? 1u : 0u, dst, true, true, true);
+    const uint32_t c = wave_crc(T, src, size, 1u, comp ? 1u : 0u, dst, true, true, true);
     const uint32_t m = crc_mask(c);                                   // :142
     if (lane_id() < 4) dst[size + 1 + lane_id()] = (uint8_t)(m >> (8 * lane_id()));
     if (lane_id() == 0) {
@@ -449,7 +430,6 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     uint64_t* __restrict__ dec_off, uint32_t* __restrict__ dec_cap, uint64_t dummy_off,
     uint32_t n) {
   __shared__ uint32_t s_tab[kTabWords];
-  __shared__ __attribute__((aligned(16))) uint32_t s_img[WAVES][kImgWords];
   load_tables(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
@@ -475,11 +455,11 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
       if (verify) {                                                   // :203-211
         const uint32_t stored = (uint32_t)data[sz + 1] | ((uint32_t)data[sz + 2] << 8) |
                                 ((uint32_t)data[sz + 3] << 16) | ((uint32_t)data[sz + 4] << 24);
-        const uint32_t c = wave_crc(T, s_img[wv], data, sz, 1u, ty, to_global(out) + oo,
+        const uint32_t c = wave_crc(T, data, sz, 1u, ty, to_global(out) + oo,
                                     raw_fits, false, true);
         ok = crc_unmask(uni(stored)) == c;
       } else if (raw_fits) {
-        wave_crc(T, s_img[wv], data, sz, 0u, 0u, to_global(out) + oo, true, false, false);
+        wave_crc(T, data, sz, 0u, 0u, to_global(out) + oo, true, false, false);
       }
       if (!ok) {
         st = kStBadCrc;
@@ -519,7 +499,7 @@ __global__ __launch_bounds__(256) void merge_kernel(uint8_t* __restrict__ status
 // resident at once (CUs x the occupancy the kernel's LDS allows), each
 // loading the tables once and striding over blocks -- no second, partial
 // round of workgroups.
-constexpr uint32_t kFrameWaves = 4;
+constexpr uint32_t kFrameWaves = 8;
 template <class K>
 uint32_t frame_grid(K kernel, uint32_t n) {
   static uint32_t resident = 0;   // same on every device of the node

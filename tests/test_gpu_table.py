@@ -55,7 +55,7 @@ def _crc_cases():
     return cases
 
 
-@pytest.mark.parametrize("shift", [0, 3])
+@pytest.mark.parametrize("shift", [0, 1, 3, 4, 6, 8, 13, 15])
 @pytest.mark.parametrize("with_type", [False, True])
 def test_crc32c_batch_vs_oracle(tab, shift, with_type):
     import torch
@@ -77,6 +77,43 @@ def test_crc32c_batch_vs_oracle(tab, shift, with_type):
         got = tab.crc32c_batch(buf, off, ln, None, False).cpu().numpy().astype(np.uint32)
         assert [int(x) for x in got[:6]] == [0x8a9136aa, 0x62a8ab43, 0x46dd794e, 0x113fdb5c,
                                              0xd9963a56, 0xb0d7025a]
+
+
+def test_crc32c_flush_with_allocation_end(tab):
+    # Blocks whose last byte is the last byte of a device mapping followed by
+    # an unmapped granule: the CRC reads only granules holding block bytes
+    # (the type byte comes from its own array), so none of these faults.
+    import ctypes as C
+    import torch
+    from test_gpu_parity import _guarded_page
+    hip = C.CDLL("libamdhip64.so")
+    rng = random.Random(0x9a4d)
+    lengths = [1, 3, 4, 15, 16, 17, 63, 64, 65, 4095, 4096, 4097, 9000]
+    base, size, release = _guarded_page(hip, 9000 + 64)
+    try:
+        for L in lengths:
+            raw = rng.randbytes(L)
+            src = np.frombuffer(raw, dtype=np.uint8)
+            assert hip.hipMemcpy(C.c_void_p(base + size - L), C.c_void_p(src.ctypes.data),
+                                 C.c_size_t(L), 1) == 0
+            off = torch.tensor([size - L], dtype=torch.int64, device="cuda")
+            ln = torch.tensor([L], dtype=torch.int32, device="cuda")
+            ty = torch.tensor([1], dtype=torch.uint8, device="cuda")
+            crc = torch.zeros(1, dtype=torch.int32, device="cuda")
+            for d_type in (None, ty):
+                s = torch.cuda.current_stream()
+                tab.check(tab._L.lgs_crc32c_batch_dev(
+                    C.c_void_p(base), off.data_ptr(), ln.data_ptr(),
+                    d_type.data_ptr() if d_type is not None else None, 0, crc.data_ptr(), 1,
+                    s.cuda_stream), "lgs_crc32c_batch_dev")
+                s.synchronize()
+                want = oracle.crc32c(raw)
+                if d_type is not None:
+                    want = oracle.crc32c(b"\x01", want)
+                assert int(crc.item()) & 0xffffffff == want, (L, d_type is not None)
+    finally:
+        torch.cuda.synchronize()
+        release()
 
 
 @pytest.fixture(scope="module")

@@ -24,7 +24,7 @@ def main() -> None:
     if stats:
         for r in csv.DictReader(open(stats[0])):
             if "lgs::" in r["Name"]:
-                k = r["Name"].split("(")[0].replace("void ", "")
+                k = r["Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
                 out.setdefault(k, {})["avg_us"] = float(r["AverageNs"]) / 1e3
                 out[k]["calls"] = int(r["Calls"])
     for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
@@ -32,7 +32,7 @@ def main() -> None:
         for r in csv.DictReader(open(f)):
             if "lgs::" not in r["Kernel_Name"]:
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, cs in agg.items():
             for c, v in cs.items():
