@@ -13,24 +13,23 @@
 // CRC on a wave (one block per wave, any length).  CRC32C is linear over
 // GF(2), so the wave splits a block into 64-byte segments, one per lane,
 // and combines them:
-//  * the block is virtually left-padded with zeros to a multiple of 4096
-//    bytes (a 4096-byte "pass" = 64 lanes x 64 bytes).  Leading zeros do not
-//    change the unconditioned CRC (register 0 stays 0), and the ~0
-//    pre-conditioning equals complementing the message's first 4 bytes, so
-//    every pass is 64 equal segments and every lane does identical work;
-//  * a lane loads the aligned 16-byte granules under its segment (only
-//    granules holding a byte of the block: never another page) and shifts
-//    them into place in registers by the pass's misalignment, which is the
-//    same for every lane (no LDS image);
+//  * the block's bytes are taken where they lie, as the aligned 16-byte
+//    granules that hold them (only those: never another page), extended by
+//    t < 16 trailing zeros to the end of the last granule and by leading
+//    zeros to a multiple of 4096 bytes (a "pass" = 64 lanes x 64 bytes).
+//    Leading zeros leave a register that is 0 at 0; the ~0
+//    pre-conditioning is the start register of the lane holding byte 0
+//    (the register that its leading zeros turn into ~0); the trailing
+//    zeros are divided out at the end (a multiplication by x^(-8t));
 //  * a lane folds its 16 dwords with slice-by-4 tables (4 LDS lookups per
 //    dword), then multiplies its CRC by x^(512 (63 - lane)) -- the zero
 //    bytes after its segment -- with a table of its own (eight nibble
 //    lookups), and one xor-reduction over the wave (DPP) gives the pass's
 //    CRC.  The CRC of the passes before enters as lane 0's start register.
-// A lane's registers also feed the copy to the destination (the file image
-// on the write path, the output slot of a raw block on the read path): its
-// whole 16-byte chunks are stored as they are, the first 16 bytes of the
-// block (and, without its type byte, the last 16) by one lane each.
+// A lane's granules also feed the copy to the destination (the file image
+// on the write path, the output slot of a raw block on the read path):
+// whole 16-byte chunks of the block are stored as they are, the first and
+// the last 16 bytes by one lane each.
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
@@ -44,7 +43,9 @@ constexpr uint32_t kSeg = 64;                 // bytes per lane per pass
 constexpr uint32_t kPass = kSeg * kWave;      // 4096
 constexpr uint32_t kLaneBase = 1024;          // after the slice-by-4 tables
 constexpr uint32_t kLaneStride = 129;         // 128 words a lane, +1 spreads the banks
-constexpr uint32_t kTabWords = kLaneBase + kLaneStride * kWave;
+constexpr uint32_t kTabWords = kLaneBase + kLaneStride * kWave;   // copied to LDS
+constexpr uint32_t kInitBase = kTabWords;     // 64 start registers (read uniformly)
+constexpr uint32_t kInvBase = kInitBase + 64; // 16 x 128: divide by x^(8t), t < 16
 
 // a * b mod P over GF(2), reflected (bit 31 is x^0).
 constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
@@ -56,11 +57,26 @@ constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
   return p;
 }
 
-struct CrcTables {
-  uint32_t w[kTabWords];
+struct alignas(16) CrcTables {
+  uint32_t w[kInvBase + 16 * 128];
   // w[k*256 + b]          slice-by-4: byte b followed by k zero bytes
   // w[1024 + 129*L + 16j + v]  (v << 4j) times x^(512 * (63 - L)): lane L's
   //                        segment followed by the 63 - L segments after it
+  // w[kInitBase + z]       the register that z zero bytes turn into ~0
+  // w[kInvBase + 128t + 16j + v]  (v << 4j) times x^(-8t)
+  constexpr void nibbles(uint32_t* t, uint32_t m) {  // t[16j + v] = (v << 4j) * m
+    uint32_t bx[32] = {};                            // bx[i] = m * x^i
+    bx[0] = m;
+    for (int i = 1; i < 32; ++i) bx[i] = (bx[i - 1] & 1u) ? (bx[i - 1] >> 1) ^ kPoly : (bx[i - 1] >> 1);
+    for (uint32_t j = 0; j < 8; ++j) {
+      t[16 * j] = 0;
+      for (uint32_t v = 1; v < 16; ++v) {
+        uint32_t b = 0;
+        while (!((v >> b) & 1u)) ++b;
+        t[16 * j + v] = t[16 * j + (v & (v - 1))] ^ bx[31 - (4 * j + b)];  // bit 4j+b is x^(31-4j-b)
+      }
+    }
+  }
   constexpr CrcTables() : w() {
     for (uint32_t b = 0; b < 256; ++b) {
       uint32_t c = b;
@@ -76,33 +92,45 @@ struct CrcTables {
     for (int j = 0; j < 9; ++j) x512 = gf_mul(x512, x512); // x^512: 64 zero bytes
     uint32_t xp = 0x80000000u;                           // x^0 for lane 63
     for (int L = (int)kWave - 1; L >= 0; --L) {
-      uint32_t bx[32] = {};                              // bx[i] = xp * x^i
-      bx[0] = xp;
-      for (int i = 1; i < 32; ++i) bx[i] = (bx[i - 1] & 1u) ? (bx[i - 1] >> 1) ^ kPoly : (bx[i - 1] >> 1);
-      for (uint32_t j = 0; j < 8; ++j) {
-        uint32_t* t = w + kLaneBase + kLaneStride * (uint32_t)L + 16 * j;
-        t[0] = 0;
-        for (uint32_t v = 1; v < 16; ++v) {
-          uint32_t b = 0;
-          while (!((v >> b) & 1u)) ++b;
-          t[v] = t[v & (v - 1)] ^ bx[31 - (4 * j + b)];  // bit 4j+b is x^(31-4j-b)
-        }
-      }
+      nibbles(w + kLaneBase + kLaneStride * (uint32_t)L, xp);
       xp = gf_mul(xp, x512);
+    }
+    // One zero byte maps c to T[c & 255] ^ (c >> 8), whose top byte is the
+    // top byte of T[c & 255]; those 256 top bytes are distinct, so the step
+    // inverts: find the index by the top byte, then undo the xor and shift.
+    uint32_t inv_top[256] = {};
+    for (uint32_t b = 0; b < 256; ++b) inv_top[w[b] >> 24] = b;
+    uint32_t r = ~0u, m = 0x80000000u;                   // m = x^(-8t)
+    for (uint32_t z = 0; z < 64; ++z) {
+      w[kInitBase + z] = r;
+      if (z < 16) nibbles(w + kInvBase + 128 * z, m);
+      uint32_t idx = inv_top[r >> 24];
+      r = ((r ^ w[idx]) << 8) | idx;
+      idx = inv_top[m >> 24];
+      m = ((m ^ w[idx]) << 8) | idx;
     }
   }
 };
 
 __constant__ CrcTables kCrc = CrcTables();
 
+// a ^ b ^ c in one instruction (v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // The tables in LDS (one copy per workgroup).
 struct Crc {
   const uint32_t* w;
-  // Four more bytes (little-endian dword) into an unconditioned register.
-  __device__ __forceinline__ uint32_t dword(uint32_t crc, uint32_t x) const {
-    const uint32_t c = crc ^ x;
-    return w[768 + (c & 255u)] ^ w[512 + ((c >> 8) & 255u)] ^ w[256 + ((c >> 16) & 255u)] ^
-           w[c >> 24];
+  // x = crc ^ (four more bytes): the register after them, xor `next`.
+  __device__ __forceinline__ uint32_t step(uint32_t x, uint32_t next) const {
+#ifdef LGS_PROBE_CRC_NOLDS   // probe: the chain without its table reads (wrong CRCs)
+    return xor3(x, x >> 7, next) + (x >> 13);
+#endif
+    return xor3(xor3(w[768 + (x & 255u)], w[512 + ((x >> 8) & 255u)], w[256 + ((x >> 16) & 255u)]),
+                w[x >> 24], next);
   }
   __device__ __forceinline__ uint32_t byte(uint32_t crc, uint32_t b) const {
     return w[(crc ^ b) & 255u] ^ (crc >> 8);
@@ -110,15 +138,42 @@ struct Crc {
   // crc followed by 64 * (63 - lane) zero bytes.
   __device__ __forceinline__ uint32_t lane_shift(uint32_t a, uint32_t lane) const {
     const uint32_t* n = w + kLaneBase + kLaneStride * lane;
-    uint32_t r = 0;
+    uint32_t t[8];
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) r ^= n[16 * j + ((a >> (4 * j)) & 15u)];
-    return r;
+    for (uint32_t j = 0; j < 8; ++j) t[j] = n[16 * j + ((a >> (4 * j)) & 15u)];
+    return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
   }
 };
 
+// A uniform register with its last t zero bytes divided out (constant
+// memory, scalar loads).
+__device__ __forceinline__ uint32_t unshift(uint32_t a, uint32_t t) {
+  const uint32_t* n = kCrc.w + kInvBase + 128 * t;
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; ++j) r ^= n[16 * j + ((a >> (4 * j)) & 15u)];
+  return r;
+}
+
+// Every load issued before the first LDS store: one memory latency per
+// workgroup, not one per 16 bytes a thread copies.
+static_assert(kTabWords % 4 == 0, "tables copied 16 bytes at a time");
+template <uint32_t NT>
 __device__ __forceinline__ void load_tables(uint32_t* s) {
-  for (uint32_t i = threadIdx.x; i < kTabWords; i += blockDim.x) s[i] = kCrc.w[i];
+  constexpr uint32_t kQ = kTabWords / 4, kPer = (kQ + NT - 1) / NT;
+  const u32x4* g = reinterpret_cast<const u32x4*>(kCrc.w);
+  u32x4* l = reinterpret_cast<u32x4*>(s);
+  u32x4 v[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * NT;
+    v[k] = g[i < kQ ? i : 0];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * NT;
+    if (i < kQ) l[i] = v[k];
+  }
   __syncthreads();
 }
 
@@ -143,22 +198,6 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 
 typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 
-// Dword i of this lane's segment is bytes sh + 4i .. sh + 4i + 3 of its
-// five granules g (sh = 4Q + (sh & 3), Q uniform).
-template <uint32_t Q>
-__device__ __forceinline__ void funnel(const u32x4 (&g)[5], uint32_t r, uint32_t (&v)[16]) {
-  uint32_t W[20];
-#pragma unroll
-  for (uint32_t t = 0; t < 5; ++t) {
-    W[4 * t] = g[t].x;
-    W[4 * t + 1] = g[t].y;
-    W[4 * t + 2] = g[t].z;
-    W[4 * t + 3] = g[t].w;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < 16; ++i) v[i] = __builtin_amdgcn_alignbyte(W[Q + i + 1], W[Q + i], r);
-}
-
 // src[0 .. e) to dst, 16 bytes a lane per step, the ragged end as the 16
 // bytes that end at e (e >= 16; reads stay inside src[0 .. e)).
 __device__ __forceinline__ void copy_bytes(gptr<const uint8_t> src, gptr<uint8_t> dst, uint32_t e) {
@@ -166,6 +205,17 @@ __device__ __forceinline__ void copy_bytes(gptr<const uint8_t> src, gptr<uint8_t
     *(gptr<u32x4_a1>)(dst + k) = *(gptr<const u32x4_a1>)(src + k);
   if (lane_id() == 0 && (e & 15u))
     *(gptr<u32x4_a1>)(dst + (e - 16)) = *(gptr<const u32x4_a1>)(src + (e - 16));
+}
+
+// Bytes [0, n) of a granule kept, the rest zero (n <= 16).
+__device__ __forceinline__ u32x4 keep_below(uint32_t n) {
+  u32x4 m;
+#pragma unroll
+  for (uint32_t d = 0; d < 4; ++d) {
+    const uint32_t nd = n > 4 * d ? n - 4 * d : 0u;
+    m[d] = nd >= 4 ? ~0u : (nd == 0 ? 0u : ~0u >> (32 - 8 * nd));
+  }
+  return m;
 }
 
 // Conditioned CRC32C (crc32c.c:643-750) of src[0 .. len) followed by the
@@ -197,74 +247,69 @@ __device__ uint32_t wave_crc(const Crc& T, gptr<const uint8_t> src, uint32_t len
   const bool chunks = copy && !short_copy;
   if (chunks) {                                               // e > 64 >= 16: len >= 16
     if (lane == 0) *(gptr<u32x4_a1>)dst = *(gptr<const u32x4_a1>)src;
-    if (lane == 1 && e != total)                              // the type byte not copied
-      *(gptr<u32x4_a1>)(dst + (len - 16)) = *(gptr<const u32x4_a1>)(src + (len - 16));
+    if (lane == 1) *(gptr<u32x4_a1>)(dst + (len - 16)) = *(gptr<const u32x4_a1>)(src + (len - 16));
+    if (lane == 2 && e != len) dst[len] = (uint8_t)type;
   }
-  const uint32_t passes = (total + kPass - 1) / kPass;
-  const uint32_t pad = passes * kPass - total;                // leading virtual zeros
   const uint64_t s0 = (uint64_t)(uintptr_t)src;
-  uint32_t acc = 0, carry = 0;
+  const uint32_t t = (uint32_t)(0u - (uint32_t)(s0 + total)) & 15u;  // trailing zeros
+  const uint32_t vtotal = total + t;
+  const uint32_t passes = (vtotal + kPass - 1) / kPass;
+  const uint32_t pad = passes * kPass - vtotal;               // leading zeros
+  const uint64_t base = s0 - pad;                             // virtual byte 0: 16-aligned
+  // The granule holding src[0] (pass 0) and the one holding index len (the
+  // type byte's place, or the first byte after the block).
+  const uint32_t vh = pad - (uint32_t)(s0 & 15u);
+  const uint32_t lh = vh >> 6, ih = (vh >> 4) & 3u;
+  const u32x4 keep_h = ~keep_below((uint32_t)(s0 & 15u));
+  const uint64_t vt = ((s0 + len) & ~15ull) - base;
+  const uint32_t pt = (uint32_t)(vt >> 12), lt = (uint32_t)(vt >> 6) & 63u, it = (uint32_t)(vt >> 4) & 3u;
+  const uint32_t ot = (uint32_t)((s0 + len) & 15u);          // index len's byte in it
+  u32x4 keep_t = keep_below(ot), put_t = u32x4{0, 0, 0, 0};
+  if (has_type) put_t[ot >> 2] = type << (8 * (ot & 3u));
+  uint32_t acc = 0;
   for (uint32_t p = 0; p < passes; ++p) {
-    const int64_t lo = (int64_t)p * kPass - pad;              // data index of virtual byte 0
-    const int64_t k0 = lo + (int64_t)(kSeg * lane);           // data index of the segment
-    const uint64_t B = s0 + (uint64_t)lo;
-    const uint32_t sh = uni((uint32_t)B & 15u);
-    const uint64_t gb = (B & ~15ull) + (uint64_t)(kSeg * lane);
-    u32x4 g[5];
+    const uint64_t seg = base + (uint64_t)p * kPass + (uint64_t)(kSeg * lane);
+    u32x4 g[4];
 #pragma unroll
-    for (uint32_t i = 0; i < 5; ++i) {
-      const uint64_t a = gb + 16ull * i;
+    for (uint32_t i = 0; i < 4; ++i) {
+      const uint64_t a = seg + 16ull * i;
       g[i] = u32x4{0, 0, 0, 0};
+#ifdef LGS_PROBE_CRC_NOLOAD   // probe: no block bytes read (wrong CRCs, same control flow)
+      if (a + 16 > s0 && a < s0 + len) g[i] = u32x4{(uint32_t)a, (uint32_t)(a >> 7), lane, i};
+      continue;
+#endif
       if (a + 16 > s0 && a < s0 + len) g[i] = *(gptr<const u32x4>)(src + (int64_t)(a - s0));
     }
-    uint32_t v[16];
-    switch (sh >> 2) {
-      case 0: funnel<0>(g, sh & 3u, v); break;
-      case 1: funnel<1>(g, sh & 3u, v); break;
-      case 2: funnel<2>(g, sh & 3u, v); break;
-      default: funnel<3>(g, sh & 3u, v); break;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+      if (p == 0 && i == ih && lane == lh) g[i] &= keep_h;    // bytes before src[0]
+      if (p == pt && i == it && lane == lt) g[i] = (g[i] & keep_t) | put_t;
     }
-    const bool last = p + 1 == passes;
-    if (last && has_type && lane == kWave - 1) v[15] = (v[15] & 0x00ffffffu) | (type << 24);
     if (chunks) {
 #pragma unroll
-      for (uint32_t c = 0; c < 4; ++c) {
-        const int64_t k = k0 + 16 * c;
-        if (k >= 0 && k + 16 <= (int64_t)e)
-          *(gptr<u32x4_a1>)(dst + k) = u32x4{v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]};
+      for (uint32_t i = 0; i < 4; ++i) {
+        const int64_t k = (int64_t)(seg + 16ull * i - s0);    // data index of the chunk
+        if (k >= 0 && k + 16 <= (int64_t)len) *(gptr<u32x4_a1>)(dst + k) = g[i];
       }
     }
-    uint32_t lane_h = 0;
-    if (p == 0) {
-      // Lane lane_h holds data index 0 at segment byte zpos: zero what is
-      // before it (bytes of the granule before src) and complement data
-      // bytes 0..3 (the ~0 pre-conditioning), spilling into the next lane.
-      lane_h = pad >> 6;
-      const uint32_t zpos = pad & 63u, D = zpos >> 2, r = zpos & 3u;
-      const uint32_t hi_keep = ~0u << (8 * r), lo_spill = r ? ~0u >> (32 - 8 * r) : 0u;
-      if (lane == lane_h) {
-#pragma unroll
-        for (uint32_t i = 0; i < 16; ++i) {
-          const uint32_t ma = i < D ? 0u : (i == D ? hi_keep : ~0u);
-          const uint32_t mx = i == D ? hi_keep : (i == D + 1 ? lo_spill : 0u);
-          v[i] = (v[i] & ma) ^ mx;
-        }
-      }
-      if (D == 15 && lane == lane_h + 1) v[0] ^= lo_spill;
-      if (D == 15 && lane_h == kWave - 1) carry = lo_spill;   // into the next pass
-    } else if (p == 1) {
-      if (lane == 0) v[0] ^= carry;
-    }
+    // Lane lane_h holds data index 0 at segment byte pad & 63 (pass 0); the
+    // lanes before it are all padding.  Its chain starts from the register
+    // that those zero bytes turn into ~0 (the pre-conditioning); lane 0's
+    // from the CRC of the passes before.
+    const uint32_t lane_h = p == 0 ? pad >> 6 : 0u;
     uint32_t c = 0;
-    if (lane >= lane_h) {                                     // lanes before: all padding
-      c = lane == 0 ? acc : 0u;
+    if (lane >= lane_h) {
+      const uint32_t init = p == 0 ? kCrc.w[kInitBase + (pad & 63u)] : acc;
+      uint32_t x = g[0].x ^ (lane == lane_h ? init : 0u);
+      const uint32_t v[16] = {g[0].x, g[0].y, g[0].z, g[0].w, g[1].x, g[1].y, g[1].z, g[1].w,
+                              g[2].x, g[2].y, g[2].z, g[2].w, g[3].x, g[3].y, g[3].z, g[3].w};
 #pragma unroll
-      for (uint32_t i = 0; i < 16; ++i) c = T.dword(c, v[i]);
-      c = T.lane_shift(c, lane);
+      for (uint32_t i = 0; i < 16; ++i) x = T.step(x, i < 15 ? v[i + 1] : 0u);
+      c = T.lane_shift(x, lane);
     }
     acc = wave_xor(c);
   }
-  return ~acc;
+  return ~unshift(acc, t);
 }
 
 // ---- row 1: masked (or plain) CRC32C per block -------------------------
@@ -274,8 +319,8 @@ __global__ __launch_bounds__(64 * WAVES) void crc_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
     const uint32_t* __restrict__ in_len, const uint8_t* __restrict__ type,
     uint32_t masked, uint32_t* __restrict__ crc_out, uint32_t n) {
-  __shared__ uint32_t s_tab[kTabWords];
-  load_tables(s_tab);
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+  load_tables<64 * WAVES>(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
@@ -389,8 +434,8 @@ __global__ __launch_bounds__(64 * WAVES) void frame_kernel(
     const uint64_t* __restrict__ enc_off, const uint32_t* __restrict__ enc_len,
     uint8_t* __restrict__ file, uint64_t base, const uint64_t* __restrict__ foff,
     uint64_t* __restrict__ handle_off, uint64_t* __restrict__ handle_size, uint32_t n) {
-  __shared__ uint32_t s_tab[kTabWords];
-  load_tables(s_tab);
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+  load_tables<64 * WAVES>(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
@@ -429,8 +474,8 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     uint64_t* __restrict__ dec_in_off, uint32_t* __restrict__ dec_len,
     uint64_t* __restrict__ dec_off, uint32_t* __restrict__ dec_cap, uint64_t dummy_off,
     uint32_t n) {
-  __shared__ uint32_t s_tab[kTabWords];
-  load_tables(s_tab);
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
+  load_tables<64 * WAVES>(s_tab);
   const Crc T{s_tab};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {

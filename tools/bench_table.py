@@ -28,7 +28,11 @@ def main() -> None:
     p.add_argument("--blocks", type=int, default=65536)
     p.add_argument("--block-size", type=int, default=4096)
     p.add_argument("--iters", type=int, default=20)
+    p.add_argument("--lib", default=None, help="a probe build of the codec library")
     a = p.parse_args()
+    if a.lib:
+        import lcdb_amd.build as b
+        b.LIB = os.path.abspath(a.lib)
 
     import numpy as np
     import torch
