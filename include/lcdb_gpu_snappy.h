@@ -181,7 +181,11 @@ int lgs_table_write_host(const uint8_t *raw, const uint64_t *raw_off,
    d_out + d_out_off[i] (capacity d_out_cap[i]; the decoded size of a snappy
    block is its varint32 header, ldb_snappy_decode_size).  d_status[i] =
    LGS_ST_OK or the reason the reference fails; d_out_len[i] = contents
-   length when ok.  d_file must stay readable 16 bytes past file_len.
+   length when ok (the output bytes of a block that fails are unspecified).
+   With verify_checksums the CRC checks run on a second stream of the
+   library's own beside the decoder (lgs_set_option("verify_overlap", "0")
+   or LGS_VERIFY_OVERLAP=0: inside the type dispatch); the call stays
+   ordered on `stream`.  d_file must stay readable 16 bytes past file_len.
    d_scratch: lgs_table_read_scratch(n) device bytes.  Asynchronous. */
 size_t lgs_table_read_scratch(uint32_t n);
 int lgs_table_read_dev(const uint8_t *d_file, uint64_t file_len,

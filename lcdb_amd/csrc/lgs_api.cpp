@@ -942,6 +942,8 @@ Options& options_init() {
               "decoder; this library uses its default decoders\n",
               dk ? dk : "", wd0 ? wd0 : "");
 #endif
+    const char* vo = getenv("LGS_VERIFY_OVERLAP");
+    if (vo && !strcmp(vo, "0")) v->verify_overlap = 0;
     const char* ns = getenv("LGS_NO_SPLIT");
     if (ns && *ns && strcmp(ns, "0")) v->split = 0;
     return v;
@@ -1047,6 +1049,12 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "1")) g_svc_enabled = 1;
     else if (!strcmp(value, "0")) g_svc_enabled = 0;
     else return fail(LGS_EINVAL, "service '%s' (0 or 1)", value);
+    return LGS_OK;
+  }
+  if (!strcmp(name, "verify_overlap")) {   // table reads: CRC pass beside the decoder
+    if (!strcmp(value, "1")) o.verify_overlap = 1;
+    else if (!strcmp(value, "0")) o.verify_overlap = 0;
+    else return fail(LGS_EINVAL, "verify_overlap '%s' (0 or 1)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "split")) {
@@ -1266,9 +1274,10 @@ struct WriteScratch {
 };
 
 struct ReadScratch {
-  size_t in_off, len, off, cap, olen, st, dummy, total;
+  size_t in_off, len, off, cap, olen, st, bad, dummy, total;
   explicit ReadScratch(uint32_t n) {
     Layout L;
+    bad = L.take((size_t)n);
     in_off = L.take(8 * (size_t)n);
     len = L.take(4 * (size_t)n);
     off = L.take(8 * (size_t)n);
@@ -1303,6 +1312,26 @@ static int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const ui
   return LGS_OK;
 }
 
+// A second stream per device for the table reader's checksum pass.
+static hipStream_t aux_stream() {
+  static std::mutex mu;
+  static hipStream_t s[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!s[dev] && hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking) != hipSuccess)
+    s[dev] = nullptr;
+  return s[dev];
+}
+
+struct EventPair {
+  hipEvent_t e[2] = {nullptr, nullptr};
+  ~EventPair() {
+    for (hipEvent_t x : e)
+      if (x) (void)hipEventDestroy(x);   // released once the work it marks completes
+  }
+};
+
 static int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* d_hoff,
                const uint64_t* d_hsize, uint32_t n, int verify, uint8_t* d_out,
                const uint64_t* d_out_off, const uint32_t* d_out_cap, uint32_t max_out_cap,
@@ -1314,14 +1343,32 @@ static int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* 
   uint32_t* dec_cap = (uint32_t*)(scratch + R.cap);
   uint32_t* dec_olen = (uint32_t*)(scratch + R.olen);
   uint8_t* dec_st = scratch + R.st;
+  uint8_t* bad = scratch + R.bad;
   // The dummy slot as an offset from d_out (two's complement wrap).
   const uint64_t dummy_off = (uint64_t)(uintptr_t)(scratch + R.dummy) - (uint64_t)(uintptr_t)d_out;
-  CheckArgs c{d_file, file_len, d_hoff, d_hsize, verify ? 1u : 0u, d_out, d_out_off, d_out_cap,
+  // With checksums verified, the CRC pass (verify_kernel) runs on a second
+  // stream beside the type dispatch and the decoder, which do not need its
+  // result; the merge applies it first, as format.c:203-211 checks the
+  // trailer before the type.  Outputs of a block that fails are unspecified.
+  hipStream_t a = verify && options().verify_overlap.load() ? aux_stream() : nullptr;
+  EventPair ev;
+  CheckArgs c{d_file, file_len, d_hoff, d_hsize, verify && !a ? 1u : 0u, d_out, d_out_off, d_out_cap,
               d_out_len, d_status, dec_in_off, dec_len, dec_off, dec_cap, dummy_off, n};
   LGS_HIP(launch_check(c, s));
+  if (a) {
+    // After the type dispatch: queued with it, both ran slower (profiles/r6j);
+    // the event costs ~8 us before the decoder starts (profiles/r6i).
+    LGS_HIP(hipEventCreateWithFlags(&ev.e[0], hipEventDisableTiming));
+    LGS_HIP(hipEventCreateWithFlags(&ev.e[1], hipEventDisableTiming));
+    LGS_HIP(hipEventRecord(ev.e[0], s));
+    LGS_HIP(hipStreamWaitEvent(a, ev.e[0], 0));
+    LGS_HIP(launch_verify(d_file, file_len, d_hoff, d_hsize, bad, n, a));
+    LGS_HIP(hipEventRecord(ev.e[1], a));
+  }
   DecodeArgs d{d_file, dec_in_off, dec_len, d_out, dec_off, dec_cap, dec_olen, dec_st, nullptr, n, nullptr};
   LGS_HIP(launch_decode(d, max_out_cap, s));
-  LGS_HIP(launch_merge(d_status, d_out_len, dec_st, dec_olen, n, s));
+  if (a) LGS_HIP(hipStreamWaitEvent(s, ev.e[1], 0));
+  LGS_HIP(launch_merge(d_status, d_out_len, dec_st, dec_olen, a ? bad : nullptr, n, s));
   return LGS_OK;
 }
 

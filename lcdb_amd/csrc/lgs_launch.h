@@ -24,6 +24,7 @@ struct Options {
   std::atomic<int> decoder{kDecAuto};   // DecodeKernel
   std::atomic<int> split{1};            // size-class split of mixed batches
   std::atomic<int> wide{0};             // WideKernel: the decoder of the wide class
+  std::atomic<int> verify_overlap{1};   // table reads: trailer CRCs beside the decoder
 };
 Options& options();
 
@@ -190,7 +191,12 @@ hipError_t launch_pack(const uint8_t* src, const uint64_t* src_off, const uint32
                        uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s);
 hipError_t launch_check(const CheckArgs& a, hipStream_t s);
 hipError_t launch_merge(uint8_t* status, uint32_t* out_len, const uint8_t* dec_status,
-                        const uint32_t* dec_out_len, uint32_t n, hipStream_t s);
+                        const uint32_t* dec_out_len, const uint8_t* bad, uint32_t n,
+                        hipStream_t s);
+// The trailer CRC checks alone (bad[i] = 1 on a mismatch), sized to run
+// beside the ring decoder.
+hipError_t launch_verify(const uint8_t* file, uint64_t file_len, const uint64_t* hoff,
+                         const uint64_t* hsize, uint8_t* bad, uint32_t n, hipStream_t s);
 
 // ---- bloom filter (lgs_bloom.hip) ----
 

@@ -46,6 +46,10 @@ constexpr uint32_t kLaneStride = 129;         // 128 words a lane, +1 spreads th
 constexpr uint32_t kTabWords = kLaneBase + kLaneStride * kWave;   // copied to LDS
 constexpr uint32_t kInitBase = kTabWords;     // 64 start registers (read uniformly)
 constexpr uint32_t kInvBase = kInitBase + 64; // 16 x 128: divide by x^(8t), t < 16
+constexpr uint32_t kBflyBase = kInvBase + 16 * 128;  // 6 x 128: shifts by 64 * 2^k bytes
+// The small LDS image (verify_kernel): slice-by-4 and the six butterfly
+// shifts, 7 KB -- small enough to sit beside the ring decoder's 8 waves.
+constexpr uint32_t kSmallWords = 1024 + 6 * 128;
 
 // a * b mod P over GF(2), reflected (bit 31 is x^0).
 constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
@@ -58,12 +62,13 @@ constexpr uint32_t gf_mul(uint32_t a, uint32_t b) {
 }
 
 struct alignas(16) CrcTables {
-  uint32_t w[kInvBase + 16 * 128];
+  uint32_t w[kBflyBase + 6 * 128];
   // w[k*256 + b]          slice-by-4: byte b followed by k zero bytes
   // w[1024 + 129*L + 16j + v]  (v << 4j) times x^(512 * (63 - L)): lane L's
   //                        segment followed by the 63 - L segments after it
   // w[kInitBase + z]       the register that z zero bytes turn into ~0
   // w[kInvBase + 128t + 16j + v]  (v << 4j) times x^(-8t)
+  // w[kBflyBase + 128k + 16j + v]  (v << 4j) times x^(512 * 2^k)
   constexpr void nibbles(uint32_t* t, uint32_t m) {  // t[16j + v] = (v << 4j) * m
     uint32_t bx[32] = {};                            // bx[i] = m * x^i
     bx[0] = m;
@@ -95,6 +100,7 @@ struct alignas(16) CrcTables {
       nibbles(w + kLaneBase + kLaneStride * (uint32_t)L, xp);
       xp = gf_mul(xp, x512);
     }
+    for (uint32_t k = 0, xk = x512; k < 6; ++k, xk = gf_mul(xk, xk)) nibbles(w + kBflyBase + 128 * k, xk);
     // One zero byte maps c to T[c & 255] ^ (c >> 8), whose top byte is the
     // top byte of T[c & 255]; those 256 top bytes are distinct, so the step
     // inverts: find the index by the top byte, then undo the xor and shift.
@@ -121,8 +127,19 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
-// The tables in LDS (one copy per workgroup).
-struct Crc {
+// Xor of v over the wave: a prefix within each row of 16 lanes (DPP
+// row_shr 1, 2, 4, 8; lanes shifted in from outside the row read 0), then
+// the four rows' last lanes.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  return lane_val(v, 15) ^ lane_val(v, 31) ^ lane_val(v, 47) ^ lane_val(v, 63);
+}
+
+// Slice-by-4 in LDS at w[0 .. 1024).
+struct CrcSlice {
   const uint32_t* w;
   // x = crc ^ (four more bytes): the register after them, xor `next`.
   __device__ __forceinline__ uint32_t step(uint32_t x, uint32_t next) const {
@@ -135,13 +152,50 @@ struct Crc {
   __device__ __forceinline__ uint32_t byte(uint32_t crc, uint32_t b) const {
     return w[(crc ^ b) & 255u] ^ (crc >> 8);
   }
-  // crc followed by 64 * (63 - lane) zero bytes.
+};
+
+// The full image (kTabWords): each lane multiplies its segment's CRC by
+// x^(512 (63 - lane)) with its own table, then one xor over the wave.
+struct Crc : CrcSlice {
   __device__ __forceinline__ uint32_t lane_shift(uint32_t a, uint32_t lane) const {
     const uint32_t* n = w + kLaneBase + kLaneStride * lane;
     uint32_t t[8];
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j) t[j] = n[16 * j + ((a >> (4 * j)) & 15u)];
     return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+  }
+  // The pass's CRC (uniform) from every lane's segment CRC.
+  __device__ __forceinline__ uint32_t combine(uint32_t c, uint32_t lane) const {
+    return wave_xor(lane_shift(c, lane));
+  }
+};
+
+// The small image (kSmallWords): a six-level butterfly -- lane i (a multiple
+// of 2^(k+1)) joins the next 2^k lanes' CRC: c * x^(512 * 2^k) ^ c(i + 2^k).
+struct CrcSmall : CrcSlice {
+  __device__ __forceinline__ uint32_t shift(uint32_t k, uint32_t a) const {
+    const uint32_t* n = w + 1024 + 128 * k;
+    uint32_t t[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) t[j] = n[16 * j + ((a >> (4 * j)) & 15u)];
+    return xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+  }
+  __device__ __forceinline__ uint32_t combine(uint32_t c, uint32_t lane) const {
+    uint32_t o;
+    // k = 0..3 inside rows of 16 lanes (DPP row_shl: lane i reads lane i + 2^k).
+    o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x101, 0xf, 0xf, false);
+    if (!(lane & 1u)) c = shift(0, c) ^ o;
+    o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x102, 0xf, 0xf, false);
+    if (!(lane & 3u)) c = shift(1, c) ^ o;
+    o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x104, 0xf, 0xf, false);
+    if (!(lane & 7u)) c = shift(2, c) ^ o;
+    o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x108, 0xf, 0xf, false);
+    if (!(lane & 15u)) c = shift(3, c) ^ o;
+    o = (uint32_t)__shfl_down((int)c, 16);
+    if (!(lane & 31u)) c = shift(4, c) ^ o;
+    o = (uint32_t)__shfl_down((int)c, 32);
+    if (lane == 0) c = shift(5, c) ^ o;
+    return lane_val(c, 0);
   }
 };
 
@@ -177,23 +231,19 @@ __device__ __forceinline__ void load_tables(uint32_t* s) {
   __syncthreads();
 }
 
+// The small image: slice-by-4 then the butterfly shifts.
+__device__ __forceinline__ void load_small_tables(uint32_t* s) {
+  for (uint32_t i = threadIdx.x; i < kSmallWords; i += blockDim.x)
+    s[i] = kCrc.w[i < 1024 ? i : kBflyBase + (i - 1024)];
+  __syncthreads();
+}
+
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) {          // crc32c.h:46-50
   return ((c >> 15) | (c << 17)) + kMaskDelta;
 }
 __device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {        // crc32c.h:53-57
   const uint32_t r = m - kMaskDelta;
   return (r >> 17) | (r << 15);
-}
-
-// Xor of v over the wave: a prefix within each row of 16 lanes (DPP
-// row_shr 1, 2, 4, 8; lanes shifted in from outside the row read 0), then
-// the four rows' last lanes.
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
-  return lane_val(v, 15) ^ lane_val(v, 31) ^ lane_val(v, 47) ^ lane_val(v, 63);
 }
 
 typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
@@ -224,7 +274,8 @@ __device__ __forceinline__ u32x4 keep_below(uint32_t n) {
 // the type byte after it when copy_type.  want_crc == false: copy only.
 // Uniform result.  Reads only the aligned 16-byte granules holding a byte of
 // src[0 .. len).
-__device__ uint32_t wave_crc(const Crc& T, gptr<const uint8_t> src, uint32_t len,
+template <class Tab>
+__device__ uint32_t wave_crc(const Tab& T, gptr<const uint8_t> src, uint32_t len,
                              uint32_t has_type, uint32_t type, gptr<uint8_t> dst, bool copy,
                              bool copy_type, bool want_crc) {
   const uint32_t lane = lane_id();
@@ -297,17 +348,16 @@ __device__ uint32_t wave_crc(const Crc& T, gptr<const uint8_t> src, uint32_t len
     // that those zero bytes turn into ~0 (the pre-conditioning); lane 0's
     // from the CRC of the passes before.
     const uint32_t lane_h = p == 0 ? pad >> 6 : 0u;
-    uint32_t c = 0;
+    uint32_t x = 0;
     if (lane >= lane_h) {
       const uint32_t init = p == 0 ? kCrc.w[kInitBase + (pad & 63u)] : acc;
-      uint32_t x = g[0].x ^ (lane == lane_h ? init : 0u);
       const uint32_t v[16] = {g[0].x, g[0].y, g[0].z, g[0].w, g[1].x, g[1].y, g[1].z, g[1].w,
                               g[2].x, g[2].y, g[2].z, g[2].w, g[3].x, g[3].y, g[3].z, g[3].w};
+      x = v[0] ^ (lane == lane_h ? init : 0u);
 #pragma unroll
       for (uint32_t i = 0; i < 16; ++i) x = T.step(x, i < 15 ? v[i + 1] : 0u);
-      c = T.lane_shift(x, lane);
     }
-    acc = wave_xor(c);
+    acc = T.combine(x, lane);
   }
   return ~unshift(acc, t);
 }
@@ -321,7 +371,7 @@ __global__ __launch_bounds__(64 * WAVES) void crc_kernel(
     uint32_t masked, uint32_t* __restrict__ crc_out, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
   load_tables<64 * WAVES>(s_tab);
-  const Crc T{s_tab};
+  const Crc T{{s_tab}};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
     const uint32_t len = uni(in_len[i]);
@@ -436,7 +486,7 @@ __global__ __launch_bounds__(64 * WAVES) void frame_kernel(
     uint64_t* __restrict__ handle_off, uint64_t* __restrict__ handle_size, uint32_t n) {
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
   load_tables<64 * WAVES>(s_tab);
-  const Crc T{s_tab};
+  const Crc T{{s_tab}};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
     const uint32_t L = uni(raw_len[i]);
@@ -465,7 +515,7 @@ constexpr uint8_t kPending = 0xff;   // snappy block: status decided by the deco
 // to the decoder through dec_in_off/dec_len/dec_off/dec_cap (others get an
 // empty input at file offset 0 and a zero-capacity dummy slot, so the
 // decoder cannot touch their output).
-template <uint32_t WAVES>
+template <uint32_t WAVES, bool CRC>
 __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     const uint8_t* __restrict__ file, uint64_t file_len, const uint64_t* __restrict__ hoff,
     const uint64_t* __restrict__ hsize, uint32_t verify, uint8_t* __restrict__ out,
@@ -474,9 +524,11 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     uint64_t* __restrict__ dec_in_off, uint32_t* __restrict__ dec_len,
     uint64_t* __restrict__ dec_off, uint32_t* __restrict__ dec_cap, uint64_t dummy_off,
     uint32_t n) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kTabWords];
-  load_tables<64 * WAVES>(s_tab);
-  const Crc T{s_tab};
+  // Without CRC (verify == 0, or the checks run in verify_kernel) no tables:
+  // this instance holds no LDS and runs beside verify_kernel.
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[CRC ? kTabWords : 4];
+  if (CRC) load_tables<64 * WAVES>(s_tab);
+  const Crc T{{s_tab}};
   const uint32_t wv = uni(threadIdx.x >> 6);
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
     const uint64_t off = uni64(hoff[i]), size = uni64(hsize[i]);
@@ -497,7 +549,7 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
       const uint32_t ty = uni(data[sz]);
       const bool raw_fits = ty == 0 && sz <= cap;
       bool ok = true;
-      if (verify) {                                                   // :203-211
+      if (CRC && verify) {                                            // :203-211
         const uint32_t stored = (uint32_t)data[sz + 1] | ((uint32_t)data[sz + 2] << 8) |
                                 ((uint32_t)data[sz + 3] << 16) | ((uint32_t)data[sz + 4] << 24);
         const uint32_t c = wave_crc(T, data, sz, 1u, ty, to_global(out) + oo,
@@ -529,13 +581,49 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
   }
 }
 
+// The trailer checks of format.c:203-211 on their own (check_kernel then
+// runs without them): bad[i] = 1 when block i's stored CRC does not match.
+// Its 7 KB of tables let one workgroup sit on every CU beside the ring
+// decoder's eight waves (151.5 of 160 KB of LDS), so it runs while the
+// blocks decode (table_read).
+template <uint32_t WAVES>
+__global__ __launch_bounds__(64 * WAVES) void verify_kernel(
+    const uint8_t* __restrict__ file, uint64_t file_len, const uint64_t* __restrict__ hoff,
+    const uint64_t* __restrict__ hsize, uint8_t* __restrict__ bad, uint32_t n) {
+  __shared__ uint32_t s_tab[kSmallWords];
+  load_small_tables(s_tab);
+  const CrcSmall T{{s_tab}};
+  const uint32_t wv = uni(threadIdx.x >> 6);
+  for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
+    const uint64_t off = uni64(hoff[i]), size = uni64(hsize[i]);
+    uint32_t b = 0;
+    if (size <= ~0ull - kTrailer && off <= file_len && file_len - off >= size + kTrailer &&
+        size <= 0x7fffffffull) {                                      // as check_kernel
+      const gptr<const uint8_t> data = to_global(file) + off;
+      const uint32_t sz = (uint32_t)size;
+      const uint32_t ty = uni(data[sz]);
+      const uint32_t stored = (uint32_t)data[sz + 1] | ((uint32_t)data[sz + 2] << 8) |
+                              ((uint32_t)data[sz + 3] << 16) | ((uint32_t)data[sz + 4] << 24);
+      const uint32_t c = wave_crc(T, data, sz, 1u, ty, nullptr, false, false, true);
+      b = crc_unmask(uni(stored)) != c;
+    }
+    if (lane_id() == 0) bad[i] = (uint8_t)b;
+  }
+}
+
 __global__ __launch_bounds__(256) void merge_kernel(uint8_t* __restrict__ status,
                                                     uint32_t* __restrict__ out_len,
                                                     const uint8_t* __restrict__ dec_status,
                                                     const uint32_t* __restrict__ dec_out_len,
-                                                    uint32_t n) {
+                                                    const uint8_t* __restrict__ bad, uint32_t n) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n || status[i] != kPending) return;
+  if (i >= n) return;
+  if (bad && bad[i]) {            // format.c:203-211 before the type dispatch
+    status[i] = kStBadCrc;
+    out_len[i] = 0;
+    return;
+  }
+  if (status[i] != kPending) return;
   status[i] = dec_status[i];      // LGS_ST_CORRUPT / OK / NOSPACE, format.c:237-252
   out_len[i] = dec_out_len[i];
 }
@@ -545,10 +633,10 @@ __global__ __launch_bounds__(256) void merge_kernel(uint8_t* __restrict__ status
 // loading the tables once and striding over blocks -- no second, partial
 // round of workgroups.
 constexpr uint32_t kFrameWaves = 8;
+uint32_t g_res_crc = 0, g_res_pack = 0, g_res_frame = 0, g_res_check = 0, g_res_check_plain = 0;
 template <class K>
-uint32_t frame_grid(K kernel, uint32_t n) {
-  static uint32_t resident = 0;   // same on every device of the node
-  if (resident == 0) {
+uint32_t frame_grid(K kernel, uint32_t n, uint32_t& resident) {   // resident: per kernel,
+  if (resident == 0) {                                              // same on every device
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -569,7 +657,7 @@ uint32_t frame_grid(K kernel, uint32_t n) {
 hipError_t launch_crc(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                       const uint8_t* type, int masked, uint32_t* crc, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(crc_kernel<kFrameWaves>, dim3(frame_grid(crc_kernel<kFrameWaves>, n)), dim3(64 * kFrameWaves),
+  hipLaunchKernelGGL(crc_kernel<kFrameWaves>, dim3(frame_grid(crc_kernel<kFrameWaves>, n, g_res_crc)), dim3(64 * kFrameWaves),
                      0, s, in, in_off, in_len, type, (uint32_t)(masked != 0), crc, n);
   return hipGetLastError();
 }
@@ -636,14 +724,14 @@ __global__ __launch_bounds__(64 * WAVES) void pack_kernel(const uint8_t* __restr
 hipError_t launch_pack(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                        uint8_t* dst, const uint64_t* dst_off, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(pack_kernel<kFrameWaves>, dim3(frame_grid(pack_kernel<kFrameWaves>, n)),
+  hipLaunchKernelGGL(pack_kernel<kFrameWaves>, dim3(frame_grid(pack_kernel<kFrameWaves>, n, g_res_pack)),
                      dim3(64 * kFrameWaves), 0, s, src, src_off, len, dst, dst_off, n);
   return hipGetLastError();
 }
 
 hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(frame_kernel<kFrameWaves>, dim3(frame_grid(frame_kernel<kFrameWaves>, a.n)), dim3(64 * kFrameWaves), 0,
+  hipLaunchKernelGGL(frame_kernel<kFrameWaves>, dim3(frame_grid(frame_kernel<kFrameWaves>, a.n, g_res_frame)), dim3(64 * kFrameWaves), 0,
                      s, a.raw, a.raw_off, a.raw_len, a.enc, a.enc_off, a.enc_len, a.file, a.base,
                      a.foff, a.handle_off, a.handle_size, a.n);
   return hipGetLastError();
@@ -651,18 +739,47 @@ hipError_t launch_frame(const FrameArgs& a, hipStream_t s) {
 
 hipError_t launch_check(const CheckArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(check_kernel<kFrameWaves>, dim3(frame_grid(check_kernel<kFrameWaves>, a.n)), dim3(64 * kFrameWaves), 0,
-                     s, a.file, a.file_len, a.hoff, a.hsize, a.verify, a.out, a.out_off,
-                     a.out_cap, a.out_len, a.status, a.dec_in_off, a.dec_len, a.dec_off, a.dec_cap,
-                     a.dummy_off, a.n);
+  if (a.verify) {
+    hipLaunchKernelGGL((check_kernel<kFrameWaves, true>),
+                       dim3(frame_grid(check_kernel<kFrameWaves, true>, a.n, g_res_check)),
+                       dim3(64 * kFrameWaves), 0, s, a.file, a.file_len, a.hoff, a.hsize, a.verify,
+                       a.out, a.out_off, a.out_cap, a.out_len, a.status, a.dec_in_off, a.dec_len,
+                       a.dec_off, a.dec_cap, a.dummy_off, a.n);
+  } else {
+    hipLaunchKernelGGL((check_kernel<kFrameWaves, false>),
+                       dim3(frame_grid(check_kernel<kFrameWaves, false>, a.n, g_res_check_plain)),
+                       dim3(64 * kFrameWaves), 0, s, a.file, a.file_len, a.hoff, a.hsize, a.verify,
+                       a.out, a.out_off, a.out_cap, a.out_len, a.status, a.dec_in_off, a.dec_len,
+                       a.dec_off, a.dec_cap, a.dummy_off, a.n);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_merge(uint8_t* status, uint32_t* out_len, const uint8_t* dec_status,
-                        const uint32_t* dec_out_len, uint32_t n, hipStream_t s) {
+                        const uint32_t* dec_out_len, const uint8_t* bad, uint32_t n,
+                        hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(merge_kernel, dim3((n + 255) / 256), dim3(256), 0, s, status, out_len,
-                     dec_status, dec_out_len, n);
+                     dec_status, dec_out_len, bad, n);
+  return hipGetLastError();
+}
+
+// One workgroup of 8 waves per CU: the verify pass keeps to the LDS the ring
+// decoder leaves free.
+constexpr uint32_t kVerifyWaves = 8;
+hipError_t launch_verify(const uint8_t* file, uint64_t file_len, const uint64_t* hoff,
+                         const uint64_t* hsize, uint8_t* bad, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  static uint32_t cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
+              ? (uint32_t)c : 256u;
+  }
+  const uint32_t want = (n + kVerifyWaves - 1) / kVerifyWaves;
+  hipLaunchKernelGGL(verify_kernel<kVerifyWaves>, dim3(want < cus ? want : cus),
+                     dim3(64 * kVerifyWaves), 0, s, file, file_len, hoff, hsize, bad, n);
   return hipGetLastError();
 }
 

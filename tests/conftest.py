@@ -78,4 +78,5 @@ def force():
 
     yield set_
     for name in touched:
-        _native.set_option(name, {"decoder": "auto", "split": "1", "wide": "walk", "service": "1"}[name])
+        _native.set_option(name, {"decoder": "auto", "split": "1", "wide": "walk", "service": "1",
+                             "verify_overlap": "1"}[name])

@@ -196,8 +196,12 @@ def test_read_blocks_host_matches_reference(tab, ref_tables, bs, verify):
         assert res[i] == d.contents[i], i
 
 
+@pytest.mark.parametrize("overlap", ["1", "0"])
 @pytest.mark.parametrize("verify", [True, False])
-def test_read_blocks_corrupted_matches_reference(tab, ref_tables, tmp_path, verify):
+def test_read_blocks_corrupted_matches_reference(tab, ref_tables, tmp_path, verify, overlap, force):
+    # overlap: the trailer CRCs in their own pass beside the decoder (the
+    # default) or inside the type dispatch.
+    force("verify_overlap", overlap)
     path, file, d = ref_tables[4096]
     for seed in range(3):
         bad = table_io.corrupt(file, 0, d.metaindex[0], 60, 100 + seed)
@@ -212,7 +216,9 @@ def test_read_blocks_corrupted_matches_reference(tab, ref_tables, tmp_path, veri
                 assert res[i] == dd.contents[i]
 
 
-def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path):
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path, overlap, force):
+    force("verify_overlap", overlap)
     path, file, d = ref_tables[256]
     n = len(file)
     handles = [(0, n), (n - 4, 0), (n - 5, 0), (n, 0), (n + 10, 3),
@@ -227,21 +233,27 @@ def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path):
         assert res[i] == (dd.contents[i] if dd.rc[i] == LDB_OK else None)
     # Type byte 2 with a valid checksum: "bad block type" (format.c:263-267);
     # a snappy type over raw bytes: corrupt stream; too small a slot: NOSPACE.
-    blocks = [b"x" * 300, b"\x05hello", b"y" * 5000]
+    # A wrong trailer CRC wins over every later outcome (format.c:203-211):
+    # raw, bad type, snappy, too small a slot.
+    blocks = [b"x" * 300, b"\x05hello", b"y" * 5000, b"z" * 100, b"w" * 50, b"\x05hello",
+              b"v" * 5000]
+    types = [2, 1, 0, 0, 2, 1, 0]
+    wrong = [0, 0, 0, 1, 1, 1, 1]
     region = bytearray()
     offs = []
-    for b, ty in zip(blocks, [2, 1, 0]):
+    for b, ty, bad in zip(blocks, types, wrong):
         offs.append(len(region))
-        c = oracle.crc32c_mask(oracle.crc32c(bytes([ty]), oracle.crc32c(b)))
+        c = oracle.crc32c_mask(oracle.crc32c(bytes([ty]), oracle.crc32c(b))) ^ bad
         region += b + bytes([ty]) + c.to_bytes(4, "little")
     sizes = np.array([len(b) for b in blocks], dtype=np.uint64)
     offs = np.array(offs, dtype=np.uint64)
-    caps = [4096, 4096, 4096]
+    caps = [4096] * len(blocks)
     res, st = tab.read_blocks_host(bytes(region), offs, sizes, caps, True)
-    for i in range(3):
+    for i in range(len(blocks)):
         ost, ores = oracle.table_read_block(bytes(region), int(offs[i]), int(sizes[i]), True, caps[i])
         assert int(st[i]) == ost and res[i] == ores, i
-    assert list(st) == [tab.LGS_ST_BADTYPE, tab.LGS_ST_CORRUPT, tab.LGS_ST_NOSPACE]
+    assert list(st) == [tab.LGS_ST_BADTYPE, tab.LGS_ST_CORRUPT, tab.LGS_ST_NOSPACE] + \
+        [tab.LGS_ST_BADCRC] * 4
 
 
 @pytest.mark.parametrize("bs", [4096, 256, 65536])
