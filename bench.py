@@ -340,6 +340,12 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
                 "alone_us_encode_decode": alone,
                 "note": "encode and decode streams on disjoint CU sets (the same decode CUs "
                         "in every XCD), the split whose slower kernel alone is fastest"}
+            # Release the masked queues: later legs' streams must not land on them.
+            import ctypes as C
+            hip = C.CDLL("libamdhip64.so")
+            torch.cuda.synchronize()
+            for st in (s_enc, s_dec):
+                hip.hipStreamDestroy(C.c_void_p(st.cuda_stream))
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))

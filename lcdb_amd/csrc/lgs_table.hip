@@ -26,10 +26,9 @@
 //    bytes after its segment -- with a table of its own (eight nibble
 //    lookups), and one xor-reduction over the wave (DPP) gives the pass's
 //    CRC.  The CRC of the passes before enters as lane 0's start register.
-// A lane's granules also feed the copy to the destination (the file image
-// on the write path, the output slot of a raw block on the read path):
-// whole 16-byte chunks of the block are stored as they are, the first and
-// the last 16 bytes by one lane each.
+// Copies to the destination (the file image on the write path, the output
+// slot of a raw block on the read path) are a pass of their own over whole
+// aligned destination granules (copy_bytes).
 #include "lgs_device.h"
 #include "lgs_launch.h"
 
@@ -248,12 +247,18 @@ __device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {        // crc32c.h:
 
 typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 
-// src[0 .. e) to dst, 16 bytes a lane per step, the ragged end as the 16
-// bytes that end at e (e >= 16; reads stay inside src[0 .. e)).
+// src[0 .. e) to dst (e >= 16): whole aligned 16-byte granules of the
+// destination, 1 KB per wave step, each read as 16 unaligned bytes of src;
+// the ragged first and last granules as the 16 bytes that start at dst and
+// end at dst + e (overlapping stores of equal bytes).  Reads stay inside
+// src[0 .. e).
 __device__ __forceinline__ void copy_bytes(gptr<const uint8_t> src, gptr<uint8_t> dst, uint32_t e) {
-  for (uint32_t k = 16 * lane_id(); k + 16 <= e; k += 16 * kWave)
-    *(gptr<u32x4_a1>)(dst + k) = *(gptr<const u32x4_a1>)(src + k);
-  if (lane_id() == 0 && (e & 15u))
+  const uint64_t d0 = (uint64_t)(uintptr_t)dst;
+  const uint32_t a = (uint32_t)((16u - (d0 & 15u)) & 15u);   // first aligned granule
+  for (uint32_t k = a + 16 * lane_id(); k + 16 <= e; k += 16 * kWave)
+    *(gptr<u32x4>)(dst + k) = *(gptr<const u32x4_a1>)(src + k);
+  if (lane_id() == 0 && a) *(gptr<u32x4_a1>)dst = *(gptr<const u32x4_a1>)src;
+  if (lane_id() == 1 && ((d0 + e) & 15u))
     *(gptr<u32x4_a1>)(dst + (e - 16)) = *(gptr<const u32x4_a1>)(src + (e - 16));
 }
 
@@ -268,38 +273,31 @@ __device__ __forceinline__ u32x4 keep_below(uint32_t n) {
   return m;
 }
 
+// src[0 .. len) to dst: a byte a lane up to 64 bytes, else copy_bytes.
+__device__ __forceinline__ void copy_block(gptr<const uint8_t> src, gptr<uint8_t> dst, uint32_t len) {
+  if (len > kWave) {
+    copy_bytes(src, dst, len);
+  } else if (lane_id() < len) {
+    dst[lane_id()] = src[lane_id()];
+  }
+}
+
 // Conditioned CRC32C (crc32c.c:643-750) of src[0 .. len) followed by the
 // byte `type` when has_type -- the trailer CRC of table_builder.c:139-140
-// before masking.  When `copy`, src[0 .. len) is also written to dst, and
-// the type byte after it when copy_type.  want_crc == false: copy only.
-// Uniform result.  Reads only the aligned 16-byte granules holding a byte of
-// src[0 .. len).
+// before masking.  Uniform result.  Reads only the aligned 16-byte granules
+// holding a byte of src[0 .. len).  (Copies are a pass of their own,
+// copy_block: the CRC pass storing its chunks cost 8-16 us more on C2's
+// framing, profiles/r6m.)
 template <class Tab>
-__device__ uint32_t wave_crc(const Tab& T, gptr<const uint8_t> src, uint32_t len,
-                             uint32_t has_type, uint32_t type, gptr<uint8_t> dst, bool copy,
-                             bool copy_type, bool want_crc) {
+__device__ __forceinline__ uint32_t wave_crc(const Tab& T, gptr<const uint8_t> src, uint32_t len,
+                             uint32_t has_type, uint32_t type) {
   const uint32_t lane = lane_id();
   const uint32_t total = len + has_type;                      // message length L'
-  const uint32_t e = len + (copy_type ? has_type : 0u);       // bytes copied
-  const bool short_copy = e <= kWave;
-  if (copy && short_copy) {                                   // a byte a lane
-    if (lane < e) dst[lane] = lane < len ? src[lane] : (uint8_t)type;
-  }
-  if (!want_crc) {
-    if (copy && !short_copy) copy_bytes(src, dst, len);       // (copy_type unused here)
-    return 0;
-  }
   if (total < 4) {                                            // tiny: one byte at a time
     uint32_t c = ~0u;
     for (uint32_t k = 0; k < len; ++k) c = T.byte(c, src[k]);
     if (has_type) c = T.byte(c, type);
     return ~c;
-  }
-  const bool chunks = copy && !short_copy;
-  if (chunks) {                                               // e > 64 >= 16: len >= 16
-    if (lane == 0) *(gptr<u32x4_a1>)dst = *(gptr<const u32x4_a1>)src;
-    if (lane == 1) *(gptr<u32x4_a1>)(dst + (len - 16)) = *(gptr<const u32x4_a1>)(src + (len - 16));
-    if (lane == 2 && e != len) dst[len] = (uint8_t)type;
   }
   const uint64_t s0 = (uint64_t)(uintptr_t)src;
   const uint32_t t = (uint32_t)(0u - (uint32_t)(s0 + total)) & 15u;  // trailing zeros
@@ -336,13 +334,6 @@ __device__ uint32_t wave_crc(const Tab& T, gptr<const uint8_t> src, uint32_t len
       if (p == 0 && i == ih && lane == lh) g[i] &= keep_h;    // bytes before src[0]
       if (p == pt && i == it && lane == lt) g[i] = (g[i] & keep_t) | put_t;
     }
-    if (chunks) {
-#pragma unroll
-      for (uint32_t i = 0; i < 4; ++i) {
-        const int64_t k = (int64_t)(seg + 16ull * i - s0);    // data index of the chunk
-        if (k >= 0 && k + 16 <= (int64_t)len) *(gptr<u32x4_a1>)(dst + k) = g[i];
-      }
-    }
     // Lane lane_h holds data index 0 at segment byte pad & 63 (pass 0); the
     // lanes before it are all padding.  Its chain starts from the register
     // that those zero bytes turn into ~0 (the pre-conditioning); lane 0's
@@ -376,8 +367,7 @@ __global__ __launch_bounds__(64 * WAVES) void crc_kernel(
   for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += gridDim.x * WAVES) {
     const uint32_t len = uni(in_len[i]);
     const uint32_t ty = type ? uni(type[i]) : 0u;
-    const uint32_t c = wave_crc(T, to_global(in) + uni64(in_off[i]), len,
-                                type ? 1u : 0u, ty, nullptr, false, false, true);
+    const uint32_t c = wave_crc(T, to_global(in) + uni64(in_off[i]), len, type ? 1u : 0u, ty);
     if (lane_id() == 0) crc_out[i] = masked ? crc_mask(c) : c;
   }
 }
@@ -497,7 +487,9 @@ __global__ __launch_bounds__(64 * WAVES) void frame_kernel(
                                          : to_global(raw) + uni64(raw_off[i]);
     const uint64_t at = uni64(foff[i]);
     const gptr<uint8_t> dst = to_global(file) + (at - base);
-    const uint32_t c = wave_crc(T, src, size, 1u, comp ? 1u : 0u, dst, true, true, true);
+    const uint32_t c = wave_crc(T, src, size, 1u, comp ? 1u : 0u);
+    copy_block(src, dst, size);
+    if (lane_id() == 0) dst[size] = (uint8_t)(comp ? 1u : 0u);
     const uint32_t m = crc_mask(c);                                   // :142
     if (lane_id() < 4) dst[size + 1 + lane_id()] = (uint8_t)(m >> (8 * lane_id()));
     if (lane_id() == 0) {
@@ -552,12 +544,10 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
       if (CRC && verify) {                                            // :203-211
         const uint32_t stored = (uint32_t)data[sz + 1] | ((uint32_t)data[sz + 2] << 8) |
                                 ((uint32_t)data[sz + 3] << 16) | ((uint32_t)data[sz + 4] << 24);
-        const uint32_t c = wave_crc(T, data, sz, 1u, ty, to_global(out) + oo,
-                                    raw_fits, false, true);
+        const uint32_t c = wave_crc(T, data, sz, 1u, ty);
         ok = crc_unmask(uni(stored)) == c;
-      } else if (raw_fits) {
-        wave_crc(T, data, sz, 0u, 0u, to_global(out) + oo, true, false, false);
       }
+      if (raw_fits) copy_block(data, to_global(out) + oo, sz);   // (unspecified if the CRC fails)
       if (!ok) {
         st = kStBadCrc;
       } else if (ty == 0) {                                           // :213-231
@@ -604,7 +594,7 @@ __global__ __launch_bounds__(64 * WAVES) void verify_kernel(
       const uint32_t ty = uni(data[sz]);
       const uint32_t stored = (uint32_t)data[sz + 1] | ((uint32_t)data[sz + 2] << 8) |
                               ((uint32_t)data[sz + 3] << 16) | ((uint32_t)data[sz + 4] << 24);
-      const uint32_t c = wave_crc(T, data, sz, 1u, ty, nullptr, false, false, true);
+      const uint32_t c = wave_crc(T, data, sz, 1u, ty);
       b = crc_unmask(uni(stored)) != c;
     }
     if (lane_id() == 0) bad[i] = (uint8_t)b;
