@@ -957,6 +957,10 @@ int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 
 Options& options() { return options_init(); }
 
+// off[i] = i * stride (lgs_table.hip; declared here, not in lgs_launch.h,
+// whose text keys the codec kernels' traffic figures).
+hipError_t launch_fill_stride(uint64_t* off, uint64_t stride, uint32_t n, hipStream_t s);
+
 }  // namespace lgs
 
 using namespace lgs;
@@ -1261,14 +1265,15 @@ namespace {
 
 // Device scratch of the write path (offsets from the scratch base).
 struct WriteScratch {
-  size_t enc_off, enc_len, part, foff, enc, total;
+  size_t enc_off, enc_len, part, foff, enc, enc_cap, total;
   WriteScratch(uint32_t n, uint64_t raw_total) {
     Layout L;
     enc_off = L.take(8 * (size_t)n);
     enc_len = L.take(4 * (size_t)n);
     part = L.take(8 * scan_parts(n) + 8);
     foff = L.take(8 * (size_t)n);
-    enc = L.take(48 * (size_t)n + raw_total + raw_total / 6 + 64);   // >= sum of 16-aligned bounds
+    enc_cap = 48 * (size_t)n + raw_total + raw_total / 6 + 64;        // >= sum of 16-aligned bounds
+    enc = L.take(enc_cap);
     total = L.at;
   }
 };
@@ -1300,7 +1305,14 @@ static int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const ui
   uint8_t* enc = scratch + W.enc;
   const bool snappy = compression == LGS_SNAPPY_COMPRESSION;
   if (snappy) {                       // table_builder.c:176-188, every block at once
-    LGS_HIP(launch_scan(0, d_raw_len, nullptr, part, 0, enc_off, nullptr, n, s));
+    // Encode slots: one stride for all when n of the largest block's bound
+    // fit (lcdb's near-uniform blocks: one fill instead of a three-kernel
+    // scan), else the scan of every block's own bound.
+    const uint64_t stride = (32 + (uint64_t)max_raw_len + max_raw_len / 6 + 15) & ~15ull;
+    if (stride * n <= W.enc_cap)
+      LGS_HIP(launch_fill_stride(enc_off, stride, n, s));
+    else
+      LGS_HIP(launch_scan(0, d_raw_len, nullptr, part, 0, enc_off, nullptr, n, s));
     EncodeArgs a{d_raw, d_raw_off, d_raw_len, enc, enc_off, enc_len, nullptr, nullptr, n, nullptr};
     LGS_HIP(launch_encode(a, max_raw_len, s));
   }

@@ -654,6 +654,18 @@ hipError_t launch_crc(const uint8_t* in, const uint64_t* in_off, const uint32_t*
 
 size_t scan_parts(uint32_t n) { return (n + kScanItems - 1) / kScanItems; }
 
+__global__ __launch_bounds__(256) void fill_stride_kernel(uint64_t* __restrict__ off,
+                                                          uint64_t stride, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) off[i] = (uint64_t)i * stride;
+}
+
+hipError_t launch_fill_stride(uint64_t* off, uint64_t stride, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_stride_kernel, dim3((n + 255) / 256), dim3(256), 0, s, off, stride, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_scan(int mode, const uint32_t* raw_len, const uint32_t* enc_len, uint64_t* part,
                        uint64_t base, uint64_t* off, uint64_t* end, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
