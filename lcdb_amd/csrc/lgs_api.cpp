@@ -1368,8 +1368,11 @@ static int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* 
               d_out_len, d_status, dec_in_off, dec_len, dec_off, dec_cap, dummy_off, n};
   LGS_HIP(launch_check(c, s));
   if (a) {
-    // After the type dispatch: queued with it, both ran slower (profiles/r6j);
-    // the event costs ~8 us before the decoder starts (profiles/r6i).
+    // After the type dispatch: queued with it, both ran slower (profiles/r6j),
+    // and queued first but sleeping through it, its workgroups took the CUs
+    // before the decoder's and left some without room for eight decoder
+    // waves (365-493 us, profiles/r6r); the event costs ~8 us before the
+    // decoder starts (profiles/r6i).
     LGS_HIP(hipEventCreateWithFlags(&ev.e[0], hipEventDisableTiming));
     LGS_HIP(hipEventCreateWithFlags(&ev.e[1], hipEventDisableTiming));
     LGS_HIP(hipEventRecord(ev.e[0], s));
