@@ -315,6 +315,13 @@ def run(a, rank: int, world: int, local: int, dist) -> None:
         cu = choose_cu_partition(
             dev_index, lambda s: batch.encode(raws[0], comps[0], s),
             lambda s: batch.decode(comps[0], outs[0], stats[0], s))
+        # Every rank runs the leg or none does (its barrier is collective).
+        have = -shard.max_over_ranks(-(1.0 if cu is not None else 0.0), dist)
+        if cu is not None and have < 1.0:
+            import ctypes as C
+            for st in cu[:2]:
+                C.CDLL("libamdhip64.so").hipStreamDestroy(C.c_void_p(st.cuda_stream))
+            cu = None
         if cu is not None:
             s_enc, s_dec, split, alone = cu
             batch.encode(raws[0], comps[0], s_enc)
