@@ -27,7 +27,7 @@ CORPUS_LIB = os.path.join(PKG, "libcorpus.so")
 PROBE_LIB = os.path.join(PKG, "liblcdb_gpu_snappy_probe.so")
 PROBE_SOURCES = ["lgs_decode_probe.hip", "lgs_decode_group.hip", "lgs_decode_chain.hip"]
 
-HIP_SOURCES = ["lgs_api.cpp", "lgs_encode.hip", "lgs_decode.hip",
+HIP_SOURCES = ["lgs_api.cpp", "lgs_encode_service.hip", "lgs_decode.hip",
                "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp", "lgs_probe.hip"]
 HIP_HEADERS = ["lgs_device.h", "lgs_launch.h", "lgs_decode_common.h", "lgs_probe_hooks.h",
                "lgs_service.h"]
@@ -36,9 +36,13 @@ EXPORTS_MAP = os.path.join(CSRC, "exports.map")
 # The files that define the two profiled codec kernels and how they are
 # launched (grid, LDS class, split); the host runtime, table and bloom
 # sources do not change what encode_kernel / decode_ring_kernel execute.
-CODEC_KERNEL_FILES = ["lgs_encode.hip", "lgs_decode.hip", "lgs_device.h", "lgs_launch.h",
+CODEC_KERNEL_FILES = ["lgs_encode.hip", "lgs_encode_service.hip", "lgs_decode.hip", "lgs_device.h", "lgs_launch.h",
                       "lgs_decode_common.h", "lgs_probe_hooks.h", "lgs_service.h"]
 ARCH = "gfx950"
+# The batch encode kernels only: LLVM's max-ILP machine scheduler (C2 encode
+# 538 -> 531 us, profiles/r6v_sched_strategy_ab.txt); the service kernel is
+# compiled without it (lgs_encode_service.hip).
+ENC_BATCH_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 # If-conversion thresholds: hipcc's defaults leave small two-way branches as
 # exec-mask regions; these fold them into selects (the ring decoder's trip:
 # 84 -> 70 s_and_saveexec regions; C2 decode 280 -> 274 us, encode unchanged,
@@ -56,7 +60,7 @@ def kernel_sources_sha() -> str:
     for name in sorted(CODEC_KERNEL_FILES):
         with open(os.path.join(CSRC, name), "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
-    h.update(" ".join(FOLD_FLAGS).encode())
+    h.update(" ".join(FOLD_FLAGS + ENC_BATCH_FLAGS).encode())
     return h.hexdigest()[:16]
 
 
@@ -80,16 +84,25 @@ def _run(cmd: list[str]) -> None:
 
 
 def build_hip(force: bool = False, extra: list[str] | None = None, out: str = LIB) -> str:
-    """The codec library; `out` / `extra` make probe builds (tools/probe_ab.py)."""
+    """The codec library; `out` / `extra` make probe builds (tools/probe_ab.py).
+    The batch encode kernels (lgs_encode.hip) are compiled on their own with
+    ENC_BATCH_FLAGS, then linked with everything else."""
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [EXPORTS_MAP,
+    enc = os.path.join(CSRC, "lgs_encode.hip")
+    deps = srcs + [enc] + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [EXPORTS_MAP,
         os.path.join(ROOT, "include", "lcdb_gpu_snappy.h")]
     if force or _stale(out, deps):
         tmp = out + ".tmp"
-        _run([_hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wextra", "-pthread", *FOLD_FLAGS, f"-Wl,--version-script={EXPORTS_MAP}", *srcs,
-              "-o", tmp, *(extra or [])])
+        obj = out + ".enc.o"
+        defines = [x for x in (extra or []) if x.startswith("-D")]
+        common = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wextra",
+                  *FOLD_FLAGS]
+        _run([_hipcc(), *common, *ENC_BATCH_FLAGS, "-DLGS_ENCODE_BATCH_ONLY", *defines, "-c", enc,
+              "-o", obj])
+        _run([_hipcc(), *common, "-shared", "-pthread", f"-Wl,--version-script={EXPORTS_MAP}",
+              *srcs, *(extra or []), "-x", "none", obj, "-o", tmp])
         os.replace(tmp, out)
+        os.remove(obj)
     return out
 
 

@@ -770,6 +770,7 @@ __device__ __forceinline__ uint32_t encode_item(EncLds<IN_CAP + 112>& s, gptr<co
 // 0xffffffff for none (a later chunk of a > 64 KiB block).  One wave per
 // work item, one-wave workgroups (a static partition over persistent waves
 // balances worse).
+#ifndef LGS_ENCODE_SERVICE_ONLY
 template <uint32_t IN_CAP>
 __global__ __launch_bounds__(64) void encode_kernel(
     const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
@@ -796,6 +797,13 @@ __global__ __launch_bounds__(64) void encode_kernel(
   if (lane_id() == 0) out_len[i] = op;
 }
 
+#endif  // !LGS_ENCODE_SERVICE_ONLY
+
+// The batch kernels and the service kernel are compiled apart (build.py):
+// the batch kernels with the max-ILP machine scheduler (C2 encode -1 %), the
+// resident service wave without it (its latency, +1.8 us a call with it;
+// DESIGN 4.1).  lgs_encode_service.hip includes this file for the latter.
+#ifndef LGS_ENCODE_BATCH_ONLY
 // The drop-in service's encode waves (lgs_launch.h): wave k serves mailbox
 // k, one block of <= kSvcMaxItem bytes at a time, from its slot's arena.
 __global__ __launch_bounds__(64) void encode_service_kernel(SvcMailbox* __restrict__ mb,
@@ -818,7 +826,9 @@ hipError_t launch_encode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
   hipLaunchKernelGGL(encode_service_kernel, dim3(nslots), dim3(64), 0, s, mb, idle, activity);
   return hipGetLastError();
 }
+#endif  // !LGS_ENCODE_BATCH_ONLY
 
+#ifndef LGS_ENCODE_SERVICE_ONLY
 // The 64 KiB class with its chunk in a W-byte LDS ring (WinIn): 32 KiB +
 // the table is 37 KB, four waves per CU (the whole-chunk image, 70 KB,
 // fits two), so C3's 1 024 blocks of 64 KiB run as one generation.
@@ -923,5 +933,6 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t max_in, hipStream_t s) {
   if (max_in > kEncCap1 && (e = launch_encode_big(c, s)) != hipSuccess) return e;
   return scratch.release();
 }
+#endif  // !LGS_ENCODE_SERVICE_ONLY
 
 }  // namespace lgs
