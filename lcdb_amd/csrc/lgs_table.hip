@@ -142,9 +142,6 @@ struct CrcSlice {
   const uint32_t* w;
   // x = crc ^ (four more bytes): the register after them, xor `next`.
   __device__ __forceinline__ uint32_t step(uint32_t x, uint32_t next) const {
-#ifdef LGS_PROBE_CRC_NOLDS   // probe: the chain without its table reads (wrong CRCs)
-    return xor3(x, x >> 7, next) + (x >> 13);
-#endif
     return xor3(xor3(w[768 + (x & 255u)], w[512 + ((x >> 8) & 255u)], w[256 + ((x >> 16) & 255u)]),
                 w[x >> 24], next);
   }
@@ -323,10 +320,6 @@ __device__ __forceinline__ uint32_t wave_crc(const Tab& T, gptr<const uint8_t> s
     for (uint32_t i = 0; i < 4; ++i) {
       const uint64_t a = seg + 16ull * i;
       g[i] = u32x4{0, 0, 0, 0};
-#ifdef LGS_PROBE_CRC_NOLOAD   // probe: no block bytes read (wrong CRCs, same control flow)
-      if (a + 16 > s0 && a < s0 + len) g[i] = u32x4{(uint32_t)a, (uint32_t)(a >> 7), lane, i};
-      continue;
-#endif
       if (a + 16 > s0 && a < s0 + len) g[i] = *(gptr<const u32x4>)(src + (int64_t)(a - s0));
     }
 #pragma unroll
