@@ -535,6 +535,14 @@ struct Service {
   SvcMailbox* mb = nullptr;           // host view: encode [0, S), decode [S, 2S)
   SvcMailbox* mb_dev = nullptr;
   uint64_t* activity = nullptr;       // device, one u64 per kind
+  // Per kind and slot kInbox bytes of fine-grained device memory that the host
+  // writes through the large-BAR mapping: the waves read a request's input
+  // from HBM instead of across PCIe.  nullptr: inputs go through the arena.
+  static constexpr size_t kInbox = 8192;
+  uint8_t* inbox = nullptr;
+  uint8_t* inbox_of(int kind, uint32_t idx) {
+    return inbox ? inbox + ((size_t)kind * kSvcMaxSlots + idx) * kInbox : nullptr;
+  }
   hipStream_t stream[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
   std::atomic<bool> launched[2];
@@ -555,6 +563,22 @@ struct Service {
     mb_dev = (SvcMailbox*)dp;
     if (hipMalloc(&activity, 16) != hipSuccess) return fail(LGS_ENOMEM, "service: hipMalloc failed");
     LGS_HIP(hipMemset(activity, 0, 16));
+    {
+      // The inbox needs a host mapping of device memory: large-BAR devices only
+      // (LGS_SERVICE_INBOX=0 keeps inputs in the arena).
+      int dev = 0;
+      hipDeviceProp_t prop{};
+      const char* env = getenv("LGS_SERVICE_INBOX");
+      if ((!env || strcmp(env, "0")) && hipGetDevice(&dev) == hipSuccess &&
+          hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.isLargeBar) {
+        void* p = nullptr;
+        if (hipExtMallocWithFlags(&p, 2 * kSvcMaxSlots * kInbox, hipDeviceMallocFinegrained) ==
+            hipSuccess)
+          inbox = (uint8_t*)p;
+        else
+          (void)hipGetLastError();
+      }
+    }
     for (int k = 0; k < 2; ++k) {
       LGS_HIP(hipStreamCreateWithFlags(&stream[k], hipStreamNonBlocking));
       LGS_HIP(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
@@ -623,16 +647,31 @@ Service* svc_for(Ctx& c) {
   if (c.svc_idx >= sv->nslots) return nullptr;
   for (int k = 0; k < 2; ++k) {
     SvcMailbox* m = sv->box(k, c.svc_idx);
-    if (__atomic_load_n(&m->arena, __ATOMIC_RELAXED) == 0)
+    if (__atomic_load_n(&m->arena, __ATOMIC_RELAXED) == 0) {
+      __atomic_store_n(&m->inbox, (uint64_t)(uintptr_t)sv->inbox_of(k, c.svc_idx), __ATOMIC_RELAXED);
       __atomic_store_n(&m->arena, (uint64_t)(uintptr_t)c.h_dev, __ATOMIC_RELEASE);
+    }
   }
   return sv;
 }
 
-// Post the request already staged at kSvcIn and wait for it: *status and
+// Where a request's input goes: the slot's inbox, or the arena at kSvcIn;
+// 16 zero bytes follow it (the decoder's read slack).
+uint8_t* svc_stage(Service& sv, Ctx& c, int kind, const uint8_t* xp, uint32_t n) {
+  uint8_t* in = sv.inbox_of(kind, c.svc_idx);
+  if (!in) in = c.h_buf + kSvcIn;
+  memcpy(in, xp, n);
+  memset(in + n, 0, 16);
+  return in;
+}
+
+// Post the request staged by svc_stage and wait for it: *status and
 // *out_len as the wave reported them.
 int svc_call(Service& sv, Ctx& c, int kind, uint32_t len, uint32_t* status, uint32_t* out_len) {
   SvcMailbox* m = sv.box(kind, c.svc_idx);
+  // The inbox is write-combined device memory: its bytes must be out before
+  // the request word (x86 orders ordinary stores, not write-combined ones).
+  __builtin_ia32_sfence();
   uint32_t seq = c.svc_seq[kind] + 1;
   if (seq == 0) seq = 1;
   c.svc_seq[kind] = seq;
@@ -674,8 +713,7 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
   const uint32_t n = (uint32_t)xn;
   if (n <= kSvcMaxItem) {
     if (Service* sv = svc_for(c)) {                              // a resident wave
-      memcpy(c.h_buf + kSvcIn, xp, n);
-      memset(c.h_buf + kSvcIn + n, 0, 16);
+      svc_stage(*sv, c, 0, xp, n);
       uint32_t st = 0, olen = 0;
       LGS_TRY(svc_call(*sv, c, 0, n, &st, &olen));
       if (st != 1 || olen > bound_of(n))
@@ -826,8 +864,7 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   uint8_t* const h = c.h_buf;
   if (want <= kSvcMaxItem && (size_t)n + 16 <= kSvcOut - kSvcIn) {
     if (Service* sv = svc_for(c)) {                              // a resident wave
-      memcpy(h + kSvcIn, xp, n);
-      memset(h + kSvcIn + n, 0, 16);
+      svc_stage(*sv, c, 1, xp, n);
       uint32_t st = 0, olen = 0;
       LGS_TRY(svc_call(*sv, c, 1, n, &st, &olen));
       if (st == LGS_ST_OK && olen != want)

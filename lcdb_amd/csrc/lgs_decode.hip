@@ -293,11 +293,11 @@ __global__ __launch_bounds__(64) void decode_service_kernel(SvcMailbox* __restri
                                                             uint64_t* __restrict__ activity) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[DecBuf<kSvcMaxItem>::kBuf];
   svc_loop(mb + blockIdx.x, idle, activity,
-           [&](uint32_t len, uint64_t arena, uint32_t* status, uint32_t* out_len) {
+           [&](uint32_t len, uint64_t input, uint64_t arena, uint32_t* status, uint32_t* out_len) {
              uint8_t* a = reinterpret_cast<uint8_t*>(arena);
              len = len < kSvcOut - kSvcIn - 16 ? len : kSvcOut - kSvcIn - 16;   // (never more)
              uint32_t want = 0;
-             const uint32_t st = decode_item<kSvcMaxItem>(s_buf, to_global(a) + kSvcIn, len,
+             const uint32_t st = decode_item<kSvcMaxItem>(s_buf, to_global(reinterpret_cast<const uint8_t*>(input)), len,
                                                           to_global(a) + kSvcOut, kSvcMaxItem,
                                                           &want);
              *status = st;

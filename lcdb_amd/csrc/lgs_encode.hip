@@ -812,11 +812,11 @@ __global__ __launch_bounds__(64) void encode_service_kernel(SvcMailbox* __restri
   __shared__ __attribute__((aligned(16))) EncLds<kSvcMaxItem + 112> s;
   if (lds_addr(&s) != 0) __builtin_trap();
   svc_loop(mb + blockIdx.x, idle, activity,
-           [&](uint32_t len, uint64_t arena, uint32_t* status, uint32_t* out_len) {
+           [&](uint32_t len, uint64_t input, uint64_t arena, uint32_t* status, uint32_t* out_len) {
              uint8_t* a = reinterpret_cast<uint8_t*>(arena);
              len = len < kSvcMaxItem ? len : kSvcMaxItem;    // (the host never posts more)
-             *out_len = encode_item<kSvcMaxItem>(s, to_global(a) + kSvcIn, len, len,
-                                                 out_slot(a, kSvcOut, len));
+             *out_len = encode_item<kSvcMaxItem>(s, to_global(reinterpret_cast<const uint8_t*>(input)),
+                                                 len, len, out_slot(a, kSvcOut, len));
              *status = 1;
            });
 }

@@ -135,7 +135,8 @@ struct alignas(128) SvcMailbox {
   uint32_t aux;      // encode: the varint header value; decode: the output capacity
   uint32_t stop;     // nonzero: the wave exits
   uint64_t arena;    // device address of the slot's mapped arena
-  uint64_t pad0[5];
+  uint64_t inbox;    // nonzero: the input is here (device memory the host writes), not at arena + kSvcIn
+  uint64_t pad0[4];
   // device -> host
   uint32_t ack;      // sequence number of the last finished request
   uint32_t status;   // decode: LGS_ST_*; encode: 1

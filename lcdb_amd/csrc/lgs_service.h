@@ -13,17 +13,17 @@
 namespace lgs {
 
 // One poll: {req, len} (one 8-byte atomic load, so a request's length is
-// never torn from its number), the stop flag and the arena, each by its own
-// lane in one instruction.
+// never torn from its number), the stop flag, the arena and the inbox, each
+// by its own lane in one instruction.
 struct SvcPoll {
   uint32_t req, len, stop;
-  uint64_t arena;
+  uint64_t arena, inbox;
 };
 __device__ __forceinline__ SvcPoll svc_poll(SvcMailbox* m) {
   const uint32_t lane = lane_id();
   uint64_t v = 0;
-  if (lane < 3) {
-    uint64_t* p = reinterpret_cast<uint64_t*>(m) + lane;   // +0 {req,len}, +8 {stop,-}, +16 arena
+  if (lane < 4) {
+    uint64_t* p = reinterpret_cast<uint64_t*>(m) + lane;   // +0 {req,len}, +8 {-,stop}, +16 arena, +24 inbox
     v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -36,6 +36,9 @@ __device__ __forceinline__ SvcPoll svc_poll(SvcMailbox* m) {
   const uint32_t alo = (uint32_t)__builtin_amdgcn_readlane(lo, 2);
   const uint32_t ahi = (uint32_t)__builtin_amdgcn_readlane(hi, 2);
   r.arena = ((uint64_t)ahi << 32) | alo;
+  const uint32_t ilo = (uint32_t)__builtin_amdgcn_readlane(lo, 3);
+  const uint32_t ihi = (uint32_t)__builtin_amdgcn_readlane(hi, 3);
+  r.inbox = ((uint64_t)ihi << 32) | ilo;
   return r;
 }
 
@@ -52,7 +55,8 @@ __device__ __forceinline__ void svc_finish(SvcMailbox* m, uint32_t req, uint32_t
   }
 }
 
-// The wave's loop: serve(len, arena, &status, &out_len) for every new request
+// The wave's loop: serve(len, input, arena, &status, &out_len) for every new
+// request (input: the inbox when set, else arena + kSvcIn)
 // of mailbox m; exits on the stop flag or once the whole kernel has seen no
 // request for `idle` ticks of the 100 MHz clock (activity: the kernel's last
 // request, device memory).
@@ -68,7 +72,7 @@ __device__ __forceinline__ void svc_loop(SvcMailbox* m, uint64_t idle, uint64_t*
     if (q.stop) break;
     if (q.req != done && q.arena != 0) {
       uint32_t status = 0, out_len = 0;
-      serve(q.len, q.arena, &status, &out_len);
+      serve(q.len, q.inbox ? q.inbox : q.arena + kSvcIn, q.arena, &status, &out_len);
       svc_finish(m, q.req, status, out_len);
       done = q.req;
       last = __builtin_amdgcn_s_memrealtime();
