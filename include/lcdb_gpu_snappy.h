@@ -309,6 +309,18 @@ int lgs_filter_block_match_host(const uint8_t *block, size_t block_len,
 int lgs_dropin_footprint(size_t *pinned, size_t *device, uint32_t *slots,
                          size_t *slot_bytes);
 
+/* Stop the drop-in's resident service waves (every device), wait until they
+   have left, and send drop-in calls through the launch path (one kernel and
+   one stream synchronisation per call) until lgs_service_resume().  The
+   waves otherwise stay while calls keep coming and leave
+   LGS_SERVICE_IDLE_US (default 2 ms) after the last call from any thread;
+   an application that synchronises the whole device under sustained
+   drop-in traffic (hipDeviceSynchronize, hipFree) brackets that with these
+   two calls.  Calls in flight complete (through the launch path if the
+   waves left first); results are the same either way. */
+int lgs_service_quiesce(void);
+int lgs_service_resume(void);
+
 /* Process-wide kernel choices (A/B and tests; the defaults pick by batch):
      "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
      "wide":    "walk"  (decoder of outputs over 16 KiB: the one-tag walk)

@@ -64,6 +64,8 @@ _SIGS = {
                                               C.c_int, _vp]),
     "lgs_dropin_footprint": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
                                        C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]),
+    "lgs_service_quiesce": (C.c_int, []),
+    "lgs_service_resume": (C.c_int, []),
     "lgs_set_option": (C.c_int, [C.c_char_p, C.c_char_p]),
     "lgs_hbm_copy_dev": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     "lgs_device_count": (C.c_int, []),

@@ -36,6 +36,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -169,6 +170,7 @@ struct Ctx {
   bool fixed = false;       // a drop-in slot: arenas never grow
   uint32_t svc_idx = ~0u;   // a drop-in slot's service mailbox (kSvcMaxSlots: none)
   uint32_t svc_seq[2] = {0, 0};   // its last request per kind (encode, decode)
+  bool retired = false;     // a service request timed out: never leased again
 };
 
 // lgs_set_device() choice of the calling thread (-1: its current device).
@@ -265,7 +267,10 @@ class CtxPool {
   void release(Ctx* c) {
     {
       std::lock_guard<std::mutex> g(mu_);
-      free_[c->device].push_back(c);
+      if (c->retired)
+        --live_[c->device];               // leaked on purpose; a new one may be made
+      else
+        free_[c->device].push_back(c);
     }
     cv_.notify_one();
   }
@@ -515,6 +520,11 @@ std::atomic<int> g_svc_enabled{[] {
   return e && !strcmp(e, "0") ? 0 : 1;
 }()};
 std::atomic<bool> g_svc_shutdown{false};
+// lgs_service_quiesce() .. lgs_service_resume(): calls take the launch path.
+std::atomic<bool> g_svc_paused{false};
+// svc_call's answer for a request taken back from a stopped service: the
+// caller runs it through the launch path.
+constexpr int kSvcWithdrawn = 1;
 
 // Idle exit of the resident waves (LGS_SERVICE_IDLE_US, default 2 ms): a
 // device-wide synchronisation waits at most this long after the last call.
@@ -534,15 +544,7 @@ struct Service {
   int state = 0;                      // 0 not set up, 1 ready, -1 unavailable
   SvcMailbox* mb = nullptr;           // host view: encode [0, S), decode [S, 2S)
   SvcMailbox* mb_dev = nullptr;
-  uint64_t* activity = nullptr;       // device, one u64 per kind
-  // Per kind and slot kInbox bytes of fine-grained device memory that the host
-  // writes through the large-BAR mapping: the waves read a request's input
-  // from HBM instead of across PCIe.  nullptr: inputs go through the arena.
-  static constexpr size_t kInbox = 8192;
-  uint8_t* inbox = nullptr;
-  uint8_t* inbox_of(int kind, uint32_t idx) {
-    return inbox ? inbox + ((size_t)kind * kSvcMaxSlots + idx) * kInbox : nullptr;
-  }
+  SvcControl* ctl = nullptr;          // device, one per kind
   hipStream_t stream[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
   std::atomic<bool> launched[2];
@@ -561,26 +563,23 @@ struct Service {
     void* dp = nullptr;
     LGS_HIP(hipHostGetDevicePointer(&dp, mb, 0));
     mb_dev = (SvcMailbox*)dp;
-    if (hipMalloc(&activity, 16) != hipSuccess) return fail(LGS_ENOMEM, "service: hipMalloc failed");
-    LGS_HIP(hipMemset(activity, 0, 16));
-    {
-      // The inbox needs a host mapping of device memory: large-BAR devices only
-      // (LGS_SERVICE_INBOX=0 keeps inputs in the arena).
-      int dev = 0;
-      hipDeviceProp_t prop{};
-      const char* env = getenv("LGS_SERVICE_INBOX");
-      if ((!env || strcmp(env, "0")) && hipGetDevice(&dev) == hipSuccess &&
-          hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.isLargeBar) {
-        void* p = nullptr;
-        if (hipExtMallocWithFlags(&p, 2 * kSvcMaxSlots * kInbox, hipDeviceMallocFinegrained) ==
-            hipSuccess)
-          inbox = (uint8_t*)p;
-        else
-          (void)hipGetLastError();
-      }
-    }
+    if (hipMalloc(&ctl, 2 * sizeof(SvcControl)) != hipSuccess)
+      return fail(LGS_ENOMEM, "service: hipMalloc failed");
+    LGS_HIP(hipMemset(ctl, 0, 2 * sizeof(SvcControl)));
+    // Each kind's resident kernel on a hardware queue of its own.  Streams
+    // beyond GPU_MAX_HW_QUEUES share queues, and a queue runs its packets in
+    // order: a relaunched encode service queued behind a decode service that
+    // sustained traffic keeps alive would never start (found by
+    // test_service_busy_slot_does_not_strand_another).  A stream with a CU
+    // mask gets a new queue, never one from the shared pool; the mask here
+    // is every CU.
+    int dev = 0;
+    hipDeviceProp_t prop{};
+    LGS_HIP(hipGetDevice(&dev));
+    LGS_HIP(hipGetDeviceProperties(&prop, dev));
+    std::vector<uint32_t> cus((size_t)(prop.multiProcessorCount + 31) / 32, ~0u);
     for (int k = 0; k < 2; ++k) {
-      LGS_HIP(hipStreamCreateWithFlags(&stream[k], hipStreamNonBlocking));
+      LGS_HIP(hipExtStreamCreateWithCUMask(&stream[k], (uint32_t)cus.size(), cus.data()));
       LGS_HIP(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
       last_use[k] = 0;
       launched[k] = false;
@@ -591,10 +590,26 @@ struct Service {
     return LGS_OK;
   }
 
-  // The kernel of `kind` running, or (re)launched.  check: ask the runtime
-  // whether a launched kernel has exited (idle) even if it was seen running.
-  int ensure(int kind) {
+  // Has the kernel of `kind` finished (or never run)?  Under mu.
+  int finished(int kind, bool* gone) {
+    *gone = true;
+    if (!launched[kind]) return LGS_OK;
+    const hipError_t q = hipEventQuery(done[kind]);
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();
+      *gone = false;
+      return LGS_OK;
+    }
+    if (q != hipSuccess) LGS_HIP(q);
+    return LGS_OK;
+  }
+
+  // The kernel of `kind` running, or (re)launched -- unless the service is
+  // paused (quiesce), when *gone reports whether it has finished.
+  int ensure(int kind, bool* gone) {
     std::lock_guard<std::mutex> g(mu);
+    *gone = false;
+    if (g_svc_paused.load()) return finished(kind, gone);
     if (launched[kind]) {
       const hipError_t q = hipEventQuery(done[kind]);
       // (A pending query's hipErrorNotReady must not linger as this thread's
@@ -606,8 +621,11 @@ struct Service {
       if (q != hipSuccess) LGS_HIP(q);
     }
     const uint64_t idle = svc_idle_us() * 100;          // 100 MHz ticks
-    LGS_HIP(kind == 0 ? launch_encode_service(mb_dev, nslots, idle, activity, stream[0])
-                      : launch_decode_service(mb_dev + kSvcMaxSlots, nslots, idle, activity + 1,
+    // The previous kernel of this kind has finished (stream order): clear its
+    // closing mark for the new waves.
+    LGS_HIP(hipMemsetAsync(&ctl[kind].closing, 0, sizeof(uint64_t), stream[kind]));
+    LGS_HIP(kind == 0 ? launch_encode_service(mb_dev, nslots, idle, ctl, stream[0])
+                      : launch_decode_service(mb_dev + kSvcMaxSlots, nslots, idle, ctl + 1,
                                               stream[1]));
     LGS_HIP(hipEventRecord(done[kind], stream[kind]));
     launched[kind] = true;
@@ -626,11 +644,37 @@ void svc_stop_all() {
         __atomic_store_n(&sv->mb[i].stop, 1u, __ATOMIC_RELEASE);
 }
 
+// lgs_service_quiesce(): every service kernel stopped and finished, and
+// drop-in calls sent through the launch path until lgs_service_resume(), so
+// an embedding application's device-wide synchronisation (hipFree,
+// hipDeviceSynchronize) does not wait for resident waves under sustained
+// traffic.  A call whose request the stopped waves left unanswered takes it
+// back (svc_call) and runs it through the launch path.
+int svc_quiesce() {
+  g_svc_paused = true;
+  for (Service* sv : g_services) {
+    if (!sv) continue;
+    std::lock_guard<std::mutex> g(sv->mu);
+    if (sv->state <= 0) continue;
+    for (uint32_t i = 0; i < 2 * kSvcMaxSlots; ++i)
+      __atomic_store_n(&sv->mb[i].stop, 1u, __ATOMIC_RELEASE);
+    int rc = LGS_OK;
+    for (int k = 0; k < 2; ++k)
+      if (sv->launched[k] && hipEventSynchronize(sv->done[k]) != hipSuccess)
+        rc = fail(LGS_EINTERNAL, "service quiesce: %s", hipGetErrorString(hipGetLastError()));
+    for (uint32_t i = 0; i < 2 * kSvcMaxSlots; ++i)
+      __atomic_store_n(&sv->mb[i].stop, 0u, __ATOMIC_RELEASE);
+    for (int k = 0; k < 2; ++k) sv->launched[k] = false;
+    if (rc != LGS_OK) return rc;
+  }
+  return LGS_OK;
+}
+
 // The calling slot's service, ready, with its arena registered; nullptr
 // when the call should take the launch path.
 Service* svc_for(Ctx& c) {
   if (!g_svc_enabled.load(std::memory_order_relaxed) || g_svc_shutdown.load() ||
-      c.svc_idx >= kSvcMaxSlots || c.device < 0 || c.device >= 64)
+      g_svc_paused.load() || c.svc_idx >= kSvcMaxSlots || c.device < 0 || c.device >= 64)
     return nullptr;
   Service* sv;
   {
@@ -647,31 +691,29 @@ Service* svc_for(Ctx& c) {
   if (c.svc_idx >= sv->nslots) return nullptr;
   for (int k = 0; k < 2; ++k) {
     SvcMailbox* m = sv->box(k, c.svc_idx);
-    if (__atomic_load_n(&m->arena, __ATOMIC_RELAXED) == 0) {
-      __atomic_store_n(&m->inbox, (uint64_t)(uintptr_t)sv->inbox_of(k, c.svc_idx), __ATOMIC_RELAXED);
+    if (__atomic_load_n(&m->arena, __ATOMIC_RELAXED) == 0)
       __atomic_store_n(&m->arena, (uint64_t)(uintptr_t)c.h_dev, __ATOMIC_RELEASE);
-    }
   }
   return sv;
 }
 
-// Where a request's input goes: the slot's inbox, or the arena at kSvcIn;
-// 16 zero bytes follow it (the decoder's read slack).
-uint8_t* svc_stage(Service& sv, Ctx& c, int kind, const uint8_t* xp, uint32_t n) {
-  uint8_t* in = sv.inbox_of(kind, c.svc_idx);
-  if (!in) in = c.h_buf + kSvcIn;
+// A request's input goes to the arena at kSvcIn, 16 zero bytes after it
+// (the decoder's read slack).  (Round 5 staged it in host-written
+// fine-grained device memory for -0.8 us, and a wave read it torn with the
+// previous request's bytes: lgs_service.h.)
+void svc_stage(Ctx& c, const uint8_t* xp, uint32_t n) {
+  uint8_t* in = c.h_buf + kSvcIn;
   memcpy(in, xp, n);
   memset(in + n, 0, 16);
-  return in;
 }
 
 // Post the request staged by svc_stage and wait for it: *status and
-// *out_len as the wave reported them.
+// *out_len as the wave reported them.  kSvcWithdrawn: the service was
+// stopped (quiesce) before it answered; the request is withdrawn (its ack
+// written by the host, so no later wave serves it) and the caller takes the
+// launch path.
 int svc_call(Service& sv, Ctx& c, int kind, uint32_t len, uint32_t* status, uint32_t* out_len) {
   SvcMailbox* m = sv.box(kind, c.svc_idx);
-  // The inbox is write-combined device memory: its bytes must be out before
-  // the request word (x86 orders ordinary stores, not write-combined ones).
-  __builtin_ia32_sfence();
   uint32_t seq = c.svc_seq[kind] + 1;
   if (seq == 0) seq = 1;
   c.svc_seq[kind] = seq;
@@ -679,20 +721,33 @@ int svc_call(Service& sv, Ctx& c, int kind, uint32_t len, uint32_t* status, uint
                    __ATOMIC_RELEASE);
   const int64_t t_post = now_ns();
   // Not used for over half the idle time: its kernel has likely exited.
+  bool gone = false;
   if (!sv.launched[kind] ||
       t_post - sv.last_use[kind].load(std::memory_order_relaxed) > (int64_t)svc_idle_us() * 500)
-    LGS_TRY(sv.ensure(kind));
+    LGS_TRY(sv.ensure(kind, &gone));
   int64_t t_check = t_post;
   for (uint32_t spin = 0; __atomic_load_n(&m->ack, __ATOMIC_ACQUIRE) != seq; ++spin) {
     __builtin_ia32_pause();
-    if ((spin & 255) == 255) {
+    if (gone || (spin & 255) == 255) {
       const int64_t t = now_ns();
-      if (t - t_check > 50000) {                     // 50 us: is the kernel still there?
-        LGS_TRY(sv.ensure(kind));
+      if (gone || t - t_check > 50000) {             // 50 us: is the kernel still there?
+        if (!gone) LGS_TRY(sv.ensure(kind, &gone));
+        if (gone) {
+          // Paused and its kernel finished: answered before it left, or
+          // withdrawn now (no wave is left to write the arena).
+          if (__atomic_load_n(&m->ack, __ATOMIC_ACQUIRE) == seq) break;
+          __atomic_store_n(&m->ack, seq, __ATOMIC_RELEASE);
+          return kSvcWithdrawn;
+        }
         t_check = t;
       }
-      if (t - t_post > 20000000000ll)
+      if (t - t_post > 20000000000ll) {
+        // The wave may still answer later and write into the arena: stop it
+        // and retire the slot, so no later lessee shares the arena with it.
+        __atomic_store_n(&m->stop, 1u, __ATOMIC_RELEASE);
+        c.retired = true;
         return fail(LGS_EINTERNAL, "drop-in service: no answer in 20 s");
+      }
     }
   }
   *status = __atomic_load_n(&m->status, __ATOMIC_RELAXED);
@@ -713,14 +768,17 @@ int encode_one(uint8_t* zp, const uint8_t* xp, size_t xn, size_t* written) {
   const uint32_t n = (uint32_t)xn;
   if (n <= kSvcMaxItem) {
     if (Service* sv = svc_for(c)) {                              // a resident wave
-      svc_stage(*sv, c, 0, xp, n);
+      svc_stage(c, xp, n);
       uint32_t st = 0, olen = 0;
-      LGS_TRY(svc_call(*sv, c, 0, n, &st, &olen));
-      if (st != 1 || olen > bound_of(n))
-        return fail(LGS_EINTERNAL, "service encode: status %u, %u bytes", st, olen);
-      memcpy(zp, c.h_buf + kSvcOut, olen);
-      *written = olen;
-      return LGS_OK;
+      const int rc = svc_call(*sv, c, 0, n, &st, &olen);
+      if (rc == LGS_OK) {
+        if (st != 1 || olen > bound_of(n))
+          return fail(LGS_EINTERNAL, "service encode: status %u, %u bytes", st, olen);
+        memcpy(zp, c.h_buf + kSvcOut, olen);
+        *written = olen;
+        return LGS_OK;
+      }
+      if (rc != kSvcWithdrawn) return rc;
     }
   }
   // snappy.c:370-381: full 64 KiB chunks, then the remainder (if any);
@@ -822,15 +880,22 @@ int host_verdict(uint32_t want, size_t m) {
 // fail as if the device were out of memory.
 std::atomic<int> g_inject_alloc_failures{0};
 
-int big_alloc(uint8_t** p, size_t bytes, uint32_t want) {
+// Stream-ordered (Scratch, lgs_launch.h): freed with hipFreeAsync on the
+// slot's stream, never with hipFree, which synchronises the whole device and
+// so would wait for resident service waves.
+int big_alloc(std::unique_ptr<Scratch>* p, size_t bytes, uint32_t want, hipStream_t s) {
   unsigned wait_us = 500;
   for (int attempt = 0;; ++attempt) {
     int inj = g_inject_alloc_failures.load();
     bool injected = false;
     while (inj > 0 && !(injected = g_inject_alloc_failures.compare_exchange_weak(inj, inj - 1))) {
     }
-    if (!injected && hipMalloc(p, bytes) == hipSuccess) return LGS_OK;
-    if (!injected) (void)hipGetLastError();
+    if (!injected) {
+      p->reset(new Scratch(bytes, s));
+      if ((*p)->status() == hipSuccess) return LGS_OK;
+      p->reset();
+      (void)hipGetLastError();
+    }
     if (attempt == 12)
       return fail(LGS_ENOMEM, "hipMalloc(%zu) for a %u-byte block failed %d times", bytes, want,
                   attempt + 1);
@@ -864,14 +929,17 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   uint8_t* const h = c.h_buf;
   if (want <= kSvcMaxItem && (size_t)n + 16 <= kSvcOut - kSvcIn) {
     if (Service* sv = svc_for(c)) {                              // a resident wave
-      svc_stage(*sv, c, 1, xp, n);
+      svc_stage(c, xp, n);
       uint32_t st = 0, olen = 0;
-      LGS_TRY(svc_call(*sv, c, 1, n, &st, &olen));
-      if (st == LGS_ST_OK && olen != want)
-        return fail(LGS_EINTERNAL, "service decode: %u bytes for a %u-byte header", olen, want);
-      if (st == LGS_ST_OK) memcpy(zp, h + kSvcOut, want);
-      *ok = st == LGS_ST_OK;
-      return LGS_OK;
+      const int rc = svc_call(*sv, c, 1, n, &st, &olen);
+      if (rc == LGS_OK) {
+        if (st == LGS_ST_OK && olen != want)
+          return fail(LGS_EINTERNAL, "service decode: %u bytes for a %u-byte header", olen, want);
+        if (st == LGS_ST_OK) memcpy(zp, h + kSvcOut, want);
+        *ok = st == LGS_ST_OK;
+        return LGS_OK;
+      }
+      if (rc != kSvcWithdrawn) return rc;
     }
   }
 
@@ -914,13 +982,10 @@ int decode_one(uint8_t* zp, const uint8_t* xp, size_t xn, int* ok) {
   // device memory for this call only, the stream uploaded straight from the
   // caller's (pageable) buffer, and the output downloaded into zp only once
   // the status says ok.
-  uint8_t* big = nullptr;
+  std::unique_ptr<Scratch> guard;
   const size_t big_bytes = align_up((size_t)n + 16, 256) + align_up((size_t)want + 16, 256);
-  LGS_TRY(big_alloc(&big, big_bytes, want));
-  struct Free {
-    uint8_t* p;
-    ~Free() { (void)hipFree(p); }
-  } guard{big};
+  LGS_TRY(big_alloc(&guard, big_bytes, want, c.stream));
+  uint8_t* const big = (uint8_t*)guard->get();
   uint8_t* const d_in = big;
   uint8_t* const d_out = big + align_up((size_t)n + 16, 256);
   Layout M;                                                      // per-item arrays, in the slot
@@ -957,6 +1022,7 @@ Options& options_init() {
     const char* dk = getenv("LGS_DECODE_KERNEL");
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
+    if (dk && !strcmp(dk, "twopass")) v->decoder = kDecTwoPass;
 #ifdef LGS_PROBE_DECODERS
     if (dk && !strcmp(dk, "chain")) v->decoder = kDecChain;
     if (dk && !strcmp(dk, "group")) v->decoder = kDecGroup;
@@ -1051,6 +1117,13 @@ int lgs_dropin_footprint(size_t* pinned, size_t* device, uint32_t* slots, size_t
   return LGS_OK;
 }
 
+int lgs_service_quiesce(void) { return lgs::svc_quiesce(); }
+
+int lgs_service_resume(void) {
+  lgs::g_svc_paused = false;
+  return LGS_OK;
+}
+
 int lgs_set_option(const char* name, const char* value) {
   if (!name || !value) return fail(LGS_EINVAL, "NULL argument");
   Options& o = options();
@@ -1058,6 +1131,7 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
+    else if (!strcmp(value, "twopass")) o.decoder = kDecTwoPass;
 #ifdef LGS_PROBE_DECODERS
     else if (!strcmp(value, "chain")) o.decoder = kDecChain;
     else if (!strcmp(value, "group")) o.decoder = kDecGroup;
@@ -1066,7 +1140,7 @@ int lgs_set_option(const char* name, const char* value) {
     else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
     else if (!strcmp(value, "ops")) o.decoder = kDecOps;
 #endif
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, twopass, ring or wave)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)
@@ -1361,13 +1435,13 @@ static int table_write(const uint8_t* d_raw, const uint64_t* d_raw_off, const ui
   return LGS_OK;
 }
 
-// A second stream per device for the table reader's checksum pass.
+// A second stream per device and calling thread for the table reader's
+// checksum pass (one per device for the whole process would serialise
+// independent callers' passes on it).
 static hipStream_t aux_stream() {
-  static std::mutex mu;
-  static hipStream_t s[64] = {};
+  thread_local hipStream_t s[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
   if (!s[dev] && hipStreamCreateWithFlags(&s[dev], hipStreamNonBlocking) != hipSuccess)
     s[dev] = nullptr;
   return s[dev];

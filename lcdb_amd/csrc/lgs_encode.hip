@@ -808,10 +808,10 @@ __global__ __launch_bounds__(64) void encode_kernel(
 // k, one block of <= kSvcMaxItem bytes at a time, from its slot's arena.
 __global__ __launch_bounds__(64) void encode_service_kernel(SvcMailbox* __restrict__ mb,
                                                             uint64_t idle,
-                                                            uint64_t* __restrict__ activity) {
+                                                            SvcControl* __restrict__ ctl) {
   __shared__ __attribute__((aligned(16))) EncLds<kSvcMaxItem + 112> s;
   if (lds_addr(&s) != 0) __builtin_trap();
-  svc_loop(mb + blockIdx.x, idle, activity,
+  svc_loop(mb + blockIdx.x, idle, ctl,
            [&](uint32_t len, uint64_t input, uint64_t arena, uint32_t* status, uint32_t* out_len) {
              uint8_t* a = reinterpret_cast<uint8_t*>(arena);
              len = len < kSvcMaxItem ? len : kSvcMaxItem;    // (the host never posts more)
@@ -822,8 +822,8 @@ __global__ __launch_bounds__(64) void encode_service_kernel(SvcMailbox* __restri
 }
 
 hipError_t launch_encode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
-                                 uint64_t* activity, hipStream_t s) {
-  hipLaunchKernelGGL(encode_service_kernel, dim3(nslots), dim3(64), 0, s, mb, idle, activity);
+                                 SvcControl* ctl, hipStream_t s) {
+  hipLaunchKernelGGL(encode_service_kernel, dim3(nslots), dim3(64), 0, s, mb, idle, ctl);
   return hipGetLastError();
 }
 #endif  // !LGS_ENCODE_BATCH_ONLY

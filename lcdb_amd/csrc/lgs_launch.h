@@ -15,7 +15,8 @@ namespace lgs {
 // LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
 // launch path reads the environment).
 enum DecodeKernel {
-  kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4, kDecGroup = 5, kDecChain = 6
+  kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4, kDecGroup = 5, kDecChain = 6,
+  kDecTwoPass = 7
 };
 // Outputs over the 16 KiB class: the one-tag walk (default), or, in the
 // probe library, the trip decoder or the workgroup decoder.
@@ -64,8 +65,11 @@ hipError_t launch_decode_quad(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_ops(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s);
 #endif
-// The ring decoder (lane per block, large batches), for the split launch.
+// The ring decoder (lane per block), for the split launch and A/Bs.
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
+// The two-pass decoder (walk kernel + place kernel, outputs <= 4 608 bytes):
+// large batches of the 4 KiB class.
+hipError_t launch_decode_twopass(const DecodeArgs& a, hipStream_t s);
 #ifdef LGS_PROBE_DECODERS
 // Probe library only: the workgroup (pointer-jumping) decoder of
 // lgs_decode_group.hip, outputs up to kGroupMaxOut bytes, and the chain
@@ -119,10 +123,11 @@ class Scratch {
 // keeps one wave per drop-in slot resident instead: wave k of the encode (or
 // decode) service kernel polls mailbox k in the slot's mapped pinned memory,
 // runs the ordinary single-block walk on the slot's arena when the host posts
-// a request, and posts completion back.  A wave exits after `idle` 100 MHz
-// ticks without a request anywhere in its kernel (so a device-wide
-// synchronisation waits at most that long) or when the host sets its stop
-// flag; the host relaunches the kernel when a request finds it gone.
+// a request, and posts completion back.  The kernel's waves leave together
+// after `idle` 100 MHz ticks without a request anywhere in it (so a
+// device-wide synchronisation waits at most that long after the last call
+// from any thread), and a wave leaves when the host sets its stop flag; the
+// host relaunches the kernel when a request finds it gone.
 constexpr uint32_t kSvcMaxSlots = 64;      // mailboxes per kind
 constexpr uint32_t kSvcMaxItem = 4608;     // the 4 KiB LDS class (encode input / decode output)
 constexpr uint32_t kSvcIn = 0;             // arena offset of the request's input
@@ -135,8 +140,7 @@ struct alignas(128) SvcMailbox {
   uint32_t aux;      // encode: the varint header value; decode: the output capacity
   uint32_t stop;     // nonzero: the wave exits
   uint64_t arena;    // device address of the slot's mapped arena
-  uint64_t inbox;    // nonzero: the input is here (device memory the host writes), not at arena + kSvcIn
-  uint64_t pad0[4];
+  uint64_t pad0[5];
   // device -> host
   uint32_t ack;      // sequence number of the last finished request
   uint32_t status;   // decode: LGS_ST_*; encode: 1
@@ -145,12 +149,18 @@ struct alignas(128) SvcMailbox {
 };
 static_assert(sizeof(SvcMailbox) == 128, "mailbox layout");
 
-// nslots waves polling mb[0 .. nslots); activity: 8 bytes of device memory
-// shared by the kernel's waves (their last request, in 100 MHz ticks).
+// Device memory shared by one service kernel's waves (lgs_service.h).
+struct alignas(64) SvcControl {
+  uint64_t activity;   // the kernel's last request picked up or answered, 100 MHz ticks
+  uint64_t closing;    // nonzero: every wave leaves (set by the first idle wave; the host clears it)
+  uint64_t pad[6];
+};
+
+// nslots waves polling mb[0 .. nslots).
 hipError_t launch_encode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
-                                 uint64_t* activity, hipStream_t s);
+                                 SvcControl* ctl, hipStream_t s);
 hipError_t launch_decode_service(SvcMailbox* mb, uint32_t nslots, uint64_t idle,
-                                 uint64_t* activity, hipStream_t s);
+                                 SvcControl* ctl, hipStream_t s);
 
 // ---- SSTable block framing (lgs_table.hip) ----
 
