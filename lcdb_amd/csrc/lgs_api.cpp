@@ -1022,8 +1022,8 @@ Options& options_init() {
     const char* dk = getenv("LGS_DECODE_KERNEL");
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
-    if (dk && !strcmp(dk, "twopass")) v->decoder = kDecTwoPass;
 #ifdef LGS_PROBE_DECODERS
+    if (dk && !strcmp(dk, "twopass")) v->decoder = kDecTwoPass;
     if (dk && !strcmp(dk, "chain")) v->decoder = kDecChain;
     if (dk && !strcmp(dk, "group")) v->decoder = kDecGroup;
     const char* wg = getenv("LGS_WIDE_DECODER");
@@ -1038,7 +1038,7 @@ Options& options_init() {
     // so rather than silently measuring the default.
     const char* wd0 = getenv("LGS_WIDE_DECODER");
     if ((dk && (!strcmp(dk, "quad") || !strcmp(dk, "ops") || !strcmp(dk, "group") ||
-                !strcmp(dk, "chain"))) ||
+                !strcmp(dk, "chain") || !strcmp(dk, "twopass"))) ||
         (wd0 && (!strcmp(wd0, "trips") || !strcmp(wd0, "group"))))
       fprintf(stderr,
               "lcdb_gpu_snappy: LGS_DECODE_KERNEL=%s LGS_WIDE_DECODER=%s names a probe-library "
@@ -1131,8 +1131,8 @@ int lgs_set_option(const char* name, const char* value) {
     if (!strcmp(value, "auto") || !*value) o.decoder = kDecAuto;
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
-    else if (!strcmp(value, "twopass")) o.decoder = kDecTwoPass;
 #ifdef LGS_PROBE_DECODERS
+    else if (!strcmp(value, "twopass")) o.decoder = kDecTwoPass;
     else if (!strcmp(value, "chain")) o.decoder = kDecChain;
     else if (!strcmp(value, "group")) o.decoder = kDecGroup;
     // The decoders that lost their A/B exist in the probe library only
@@ -1140,7 +1140,7 @@ int lgs_set_option(const char* name, const char* value) {
     else if (!strcmp(value, "quad")) o.decoder = kDecQuad;
     else if (!strcmp(value, "ops")) o.decoder = kDecOps;
 #endif
-    else return fail(LGS_EINVAL, "decoder '%s' (auto, twopass, ring or wave)", value);
+    else return fail(LGS_EINVAL, "decoder '%s' (auto, ring or wave)", value);
     return LGS_OK;
   }
   if (!strcmp(name, "inject_alloc_failures")) {   // test hook (big_alloc)

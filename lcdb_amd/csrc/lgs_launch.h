@@ -67,9 +67,11 @@ hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s);
 #endif
 // The ring decoder (lane per block), for the split launch and A/Bs.
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
-// The two-pass decoder (walk kernel + place kernel, outputs <= 4 608 bytes):
-// large batches of the 4 KiB class.
+#ifdef LGS_PROBE_DECODERS
+// Probe library only: the two-pass decoder (walk kernel + place kernel,
+// outputs <= 4 608 bytes).
 hipError_t launch_decode_twopass(const DecodeArgs& a, hipStream_t s);
+#endif
 #ifdef LGS_PROBE_DECODERS
 // Probe library only: the workgroup (pointer-jumping) decoder of
 // lgs_decode_group.hip, outputs up to kGroupMaxOut bytes, and the chain

@@ -208,7 +208,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops", "group", "chain"]))
+@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops", "group", "chain", "twopass"]))
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -227,7 +227,7 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops", "group", "chain")]))
+@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops", "group", "chain", "twopass")]))
 def test_decode_kernels_c2_full_size(gpu, digests, force, kernels):
     import torch
     from lcdb_amd import batch
@@ -426,7 +426,7 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops", "group"]))
+@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops", "group", "twopass"]))
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
@@ -559,7 +559,7 @@ if PROBE:   # the two-pass decoder exists in the probe library only
 
 
 
-@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops", "group", "chain"]))
+@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops", "group", "chain", "twopass"]))
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
@@ -888,3 +888,93 @@ def test_decode_dropin_small_batch_path(gpu):
     ref = oracle.best()
     for s in _group_streams(rng, ref)[:400]:
         assert gpu.decode(s) == (ref.decode(s) if s else None)
+
+
+def _op_stream(rng, want_max=4608, max_ops=None):
+    """A valid Snappy stream built op by op (random literals and copies of
+    every tag form, overlapping and chained copies), with its output."""
+    out = bytearray()
+    body = bytearray()
+    nops = 0
+    target = rng.randrange(1, want_max + 1)
+    while len(out) < target and (max_ops is None or nops < max_ops):
+        room = target - len(out)
+        if not out or rng.random() < 0.35:
+            n = min(room, rng.choice([1, 2, 3, rng.randrange(1, 17), rng.randrange(1, 70),
+                                      rng.randrange(1, 300)]))
+            lit = bytes(rng.randrange(256) for _ in range(n))
+            m = n - 1
+            if m < 60:
+                body.append(m << 2)
+            else:
+                nb = 1 if m < 256 else 2
+                body.append((59 + nb) << 2)
+                body += m.to_bytes(nb, "little")
+            body += lit
+            out += lit
+        else:
+            n = min(room, rng.choice([rng.randrange(4, 12), rng.randrange(1, 65), 64]))
+            d = rng.choice([1, 2, 3, rng.randrange(1, 9), rng.randrange(1, len(out) + 1)])
+            d = min(d, len(out))
+            form = rng.random()
+            if 4 <= n <= 11 and d < 2048 and form < 0.4:
+                body += bytes([((d >> 8) << 5) | ((n - 4) << 2) | 1, d & 0xFF])
+            elif form < 0.9:
+                body += bytes([((n - 1) << 2) | 2]) + d.to_bytes(2, "little")
+            else:
+                body += bytes([((n - 1) << 2) | 3]) + d.to_bytes(4, "little")
+            for _ in range(n):
+                out.append(out[-d])
+        nops += 1
+    return _varint(len(out)) + bytes(body), bytes(out)
+
+
+@pytest.mark.parametrize("kernel", _with_probe(["auto", "wave"], ["twopass"]))
+def test_op_streams(gpu, force, kernel):
+    # Streams built op by op: every tag form, overlapping copies (dist < len),
+    # chains of copies of copies, streams of many tiny ops, and their
+    # truncations and corruptions -- against the reference's decode.  "auto"
+    # repeats them past the ring decoder's threshold (36 864 blocks); "wave"
+    # forces the wave decoder; the probe library's two-pass decoder
+    # (DESIGN 4.2) takes the same streams, including more tags than its walk
+    # records (its slow path).
+    import random
+    force("decoder", kernel)
+    rng = random.Random(606)
+    ref = oracle.best()
+    streams, want = [], []
+    for _ in range(600):
+        s, o = _op_stream(rng)
+        streams.append(s)
+        want.append(len(o))
+    for _ in range(20):                       # > 512 tags: the slow path
+        body = bytearray()
+        out = bytearray()
+        for k in range(rng.randrange(513, 900)):
+            if k % 2 == 0 or not out:
+                b = rng.randrange(256)
+                body += bytes([0, b])
+                out.append(b)
+            else:
+                body += bytes([((1 - 1) << 2) | 2, 1, 0])
+                out.append(out[-1])
+        streams.append(_varint(len(out)) + bytes(body))
+        want.append(len(out))
+    bad = []
+    for s in streams[:200]:
+        b = bytearray(s)
+        b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+        bad.append(bytes(b))
+        bad.append(s[:-1])
+    streams += bad
+    want += [4608] * len(bad)
+    reps = 37000 // len(streams) + 1 if kernel == "auto" else 1
+    res, st = gpu.decode_batch_host(streams * reps, want * reps)
+    for k, (s, o, code) in enumerate(zip(streams * reps, res, st)):
+        exp = ref.decode(s)
+        if exp is None or len(exp) > (want * reps)[k]:
+            assert code in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), k
+            if exp is None:
+                assert code == gpu.LGS_ST_CORRUPT, k
+        else:
+            assert code == gpu.LGS_ST_OK and o == exp, k
