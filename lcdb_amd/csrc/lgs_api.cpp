@@ -1023,7 +1023,6 @@ Options& options_init() {
     if (dk && !strcmp(dk, "ring")) v->decoder = kDecRing;
     if (dk && !strcmp(dk, "wave")) v->decoder = kDecWave;
 #ifdef LGS_PROBE_DECODERS
-    if (dk && !strcmp(dk, "twopass")) v->decoder = kDecTwoPass;
     if (dk && !strcmp(dk, "chain")) v->decoder = kDecChain;
     if (dk && !strcmp(dk, "group")) v->decoder = kDecGroup;
     const char* wg = getenv("LGS_WIDE_DECODER");
@@ -1038,7 +1037,7 @@ Options& options_init() {
     // so rather than silently measuring the default.
     const char* wd0 = getenv("LGS_WIDE_DECODER");
     if ((dk && (!strcmp(dk, "quad") || !strcmp(dk, "ops") || !strcmp(dk, "group") ||
-                !strcmp(dk, "chain") || !strcmp(dk, "twopass"))) ||
+                !strcmp(dk, "chain"))) ||
         (wd0 && (!strcmp(wd0, "trips") || !strcmp(wd0, "group"))))
       fprintf(stderr,
               "lcdb_gpu_snappy: LGS_DECODE_KERNEL=%s LGS_WIDE_DECODER=%s names a probe-library "
@@ -1132,7 +1131,6 @@ int lgs_set_option(const char* name, const char* value) {
     else if (!strcmp(value, "ring")) o.decoder = kDecRing;
     else if (!strcmp(value, "wave")) o.decoder = kDecWave;
 #ifdef LGS_PROBE_DECODERS
-    else if (!strcmp(value, "twopass")) o.decoder = kDecTwoPass;
     else if (!strcmp(value, "chain")) o.decoder = kDecChain;
     else if (!strcmp(value, "group")) o.decoder = kDecGroup;
     // The decoders that lost their A/B exist in the probe library only
@@ -1383,7 +1381,11 @@ struct WriteScratch {
     enc_len = L.take(4 * (size_t)n);
     part = L.take(8 * scan_parts(n) + 8);
     foff = L.take(8 * (size_t)n);
-    enc_cap = 48 * (size_t)n + raw_total + raw_total / 6 + 64;        // >= sum of 16-aligned bounds
+    // >= the sum of 16-aligned bounds, with 1/8 more so that near-uniform
+    // blocks (lcdb's: every one within 1/8 of the mean) take one stride
+    // (table_write: one fill kernel instead of a three-kernel scan).
+    const uint64_t bounds = raw_total + raw_total / 6;
+    enc_cap = 48 * (size_t)n + bounds + bounds / 8 + 64;
     enc = L.take(enc_cap);
     total = L.at;
   }

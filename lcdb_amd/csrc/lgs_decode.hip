@@ -1047,325 +1047,6 @@ hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s) {
 }
 
 
-#ifdef LGS_PROBE_DECODERS
-// ---------------------------------------------------------------------------
-// Two-pass decoder (round 6, probe library only: exact, and slower than the
-// ring decoder -- C2 454 against 266 us): walk, then place.  The ring decoder above walks
-// the tags and moves the bytes in one lane per block, so every instruction of
-// its trip carries the union of all op kinds' paths, at two waves per SIMD
-// (its LDS rings); its wave spends ~310 instructions per tag step
-// (DESIGN 4.2).  Here the two jobs are apart:
-//
-//  * decode_walk_kernel, one lane per block: the serial tag walk alone, from
-//    the stream in global memory (L1/L2), with every reject of
-//    snappy.c:210-338 (parse_tag) and the final length check (:337).  It
-//    writes the block's status and length -- final for every block that is
-//    not ok -- and the stream offset of each tag (u16, at most kTagCap per
-//    block; a block with more is marked for the slow path).
-//  * decode_place_kernel, one wave per block: 64 tags at a time, each lane
-//    parses its tag again (it is valid: the walk checked it), a wave scan
-//    places the ops' outputs, and the bytes move in the block's LDS image:
-//    the group's literals all at once (16 bytes a lane per step), then its
-//    copies whose source holds no byte another copy of the group writes
-//    (a per-byte mark map of the group's copy outputs) all at once, then
-//    the rest one copy at a time in stream order, 64 lanes a copy.  Then the
-//    image goes out in whole 16-byte granules.
-//
-// Outputs up to kTwoCap bytes (lcdb's 4 KiB blocks); larger classes keep
-// the other decoders.  Byte-identical to the ring decoder and the reference
-// (tests/test_gpu_parity.py forces it on every golden and corrupt stream).
-// ---------------------------------------------------------------------------
-namespace twopass {
-constexpr uint32_t kTwoCap = 4608;                 // the 4 KiB class
-constexpr uint32_t kTagCap = 512;                  // tag offset slots per block
-constexpr uint32_t kSink = kTagCap - 4;            // offsets kept (the last 4 slots: the walk's sink)
-constexpr uint32_t kSkip = 0xffffffffu;            // meta: status final, nothing to place
-constexpr uint32_t kSlow = 0xfffffffeu;            // meta: decode it from global memory
-constexpr uint32_t kImg = (16 + kTwoCap + 64 + 15) & ~15u;   // shift + image + chunk overrun
-constexpr uint32_t kMarkWords = (kTwoCap + 64) / 32 + 4;
-}  // namespace twopass
-
-__global__ __launch_bounds__(64) void decode_walk_kernel(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-    const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ out_cap,
-    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
-    const uint32_t* __restrict__ index, uint32_t n, const uint32_t* __restrict__ count,
-    uint16_t* __restrict__ tagpos, uint32_t* __restrict__ meta) {
-  using namespace twopass;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t slot = blockIdx.x * kWave + lane;
-  if (count) n = *count;
-  if (blockIdx.x * kWave >= n) return;
-  const bool exists = slot < n;
-  const uint32_t i = exists ? (index ? index[slot] : slot) : 0;
-  const gptr<const uint8_t> src = to_global(in) + (exists ? in_off[i] : 0);
-  const uint32_t slen = exists ? in_len[i] : 0;
-  const uint32_t cap = exists ? out_cap[i] : 0;
-  const gptr<uint16_t> tp = to_global(tagpos) + (size_t)i * kTagCap;
-
-  // varint32 header, coding.h:169-204; st: 1 decoding/ok, 0 corrupt, 2 no
-  // space, 3 no block.
-  uint32_t st = exists ? 1u : 3u, want = 0, hlen = 0;
-  if (exists) {
-    const uint64_t h = view8(src);
-    for (uint32_t k = 0; k < 5 && k < slen; ++k) {
-      const uint32_t b = (uint32_t)(h >> (8 * k)) & 0xffu;
-      if ((b & 0x80u) == 0) {
-        want |= b << (7 * k);
-        hlen = k + 1;
-        break;
-      }
-      want |= (b & 0x7fu) << (7 * k);
-    }
-    if (hlen == 0 || want > 0x7fffffffu) st = 0;                // snappy.c:405-409
-    else if (want > cap) st = 2;
-  }
-  // (Four offsets per 8-byte store, issued after the next tag's load and
-  // aimed at a sink slot when none is due, so the load's wait counts past
-  // it: 287 against 210 us -- the sink's partial lines took HBM writes from
-  // 23 to 302 MB, profiles/r7f_twopass_pmc.txt.)
-  uint32_t pos = hlen, made = 0, nt = 0;
-  for (;;) {                                                     // snappy.c:208
-    const bool act = (st == 1) & (pos < slen);
-    if (!ballot(act)) break;
-    const uint64_t v = view8(src + (act ? pos : 0u));
-    const Tag t = parse_tag(u32x4{(uint32_t)v, (uint32_t)(v >> 32), 0u, 0u}, pos, slen, want,
-                            made);
-    if (act & t.bad) st = 0;
-    const bool take = act & !t.bad;
-    if (take & (nt < kSink)) tp[nt] = (uint16_t)pos;
-    nt += take ? 1u : 0u;
-    made += take ? t.len : 0u;
-    pos = take ? t.next : pos;
-  }
-  if ((st == 1) & (made != want)) st = 0;                        // snappy.c:337
-  if (exists) {
-    status[i] = (uint8_t)st;
-    out_len[i] = st == 1 ? want : 0u;
-    const bool slow = (nt > kSink) | (slen > 0xffffu) | (want > kTwoCap);
-    meta[i] = st != 1 ? kSkip : (slow ? kSlow : nt);
-  }
-}
-
-// Inclusive sum over the wave: rows of 16 by DPP (row_shr 1, 2, 4, 8; lanes
-// shifted in from outside a row read 0), then the rows' totals.
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
-  const uint32_t r0 = lane_val(v, 15), r1 = lane_val(v, 31), r2 = lane_val(v, 47);
-  const uint32_t row = lane_id() >> 4;
-  return v + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
-}
-
-// The first r (< 16) bytes of v at LDS p, exactly.
-__device__ __forceinline__ void lds_put_head(uint8_t* p, u32x4 v, uint32_t r) {
-  typedef uint64_t u64_l1 __attribute__((aligned(1)));
-  typedef uint32_t u32_l1 __attribute__((aligned(1)));
-  typedef uint16_t u16_l1 __attribute__((aligned(1)));
-  if (r & 8u) {
-    *(u64_l1*)p = ((uint64_t)v.y << 32) | v.x;
-    v = u32x4{v.z, v.w, 0u, 0u};
-    p += 8;
-  }
-  if (r & 4u) {
-    *(u32_l1*)p = v.x;
-    v.x = v.y;
-    p += 4;
-  }
-  if (r & 2u) {
-    *(u16_l1*)p = (uint16_t)v.x;
-    v.x >>= 16;
-    p += 2;
-  }
-  if (r & 1u) *p = (uint8_t)v.x;
-}
-
-// Bits [a, a + len) (len <= 64) of a bit map: the dword index of the first
-// and the three dwords' masks.
-struct Span3 {
-  uint32_t w, m0, m1, m2;
-};
-__device__ __forceinline__ Span3 span3(uint32_t a, uint32_t len) {
-  const uint64_t ones = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
-  const uint32_t b = a & 31u;
-  Span3 s;
-  s.w = a >> 5;
-  s.m0 = (uint32_t)ones << b;
-  s.m1 = b ? (uint32_t)(ones >> (32 - b)) : (uint32_t)(ones >> 32);
-  s.m2 = b ? (uint32_t)(ones >> (64 - b)) : 0u;
-  return s;
-}
-
-__global__ __launch_bounds__(64) void decode_place_kernel(
-    const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-    const uint32_t* __restrict__ in_len, uint8_t* __restrict__ out,
-    const uint64_t* __restrict__ out_off, uint32_t* __restrict__ out_len,
-    uint8_t* __restrict__ status, const uint32_t* __restrict__ index, uint32_t n,
-    const uint32_t* __restrict__ count, const uint16_t* __restrict__ tagpos,
-    const uint32_t* __restrict__ meta) {
-  using namespace twopass;
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[kImg];
-  __shared__ uint32_t s_mark[kMarkWords];
-  const uint32_t lane = lane_id();
-  const uint32_t slot = blockIdx.x;
-  if (slot >= (count ? uni(*count) : n)) return;
-  const uint32_t i = uni(index ? index[slot] : slot);
-  const uint32_t ntag = uni(meta[i]);
-  if (ntag == kSkip) return;
-  const gptr<const uint8_t> src = to_global(in) + uni64(in_off[i]);
-  const gptr<uint8_t> dst = to_global(out) + uni64(out_off[i]);
-  const uint32_t oshift = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
-  uint8_t* const o = s_img + oshift;
-  if (ntag == kSlow) {
-    // Over kTagCap tags (a block of mostly tiny ops): the one-tag loop of
-    // decode_stream from global memory, into the same image.
-    const uint32_t slen = uni(in_len[i]);
-    uint32_t w = 0;
-    const uint32_t st = decode_stream(GlobalStream{src, slen}, slen, o, kTwoCap, &w);
-    order();
-    if (st == 1) flush_out(dst, s_img, w);
-    if (lane == 0) {
-      status[i] = (uint8_t)st;
-      out_len[i] = st == 1 ? w : 0u;
-    }
-    return;
-  }
-  const uint32_t want = uni(out_len[i]);
-  for (uint32_t k = lane; k < kMarkWords; k += kWave) s_mark[k] = 0;
-  const gptr<const uint16_t> tp = to_global(tagpos) + (size_t)i * kTagCap;
-
-  uint32_t made = 0;
-  for (uint32_t g0 = 0; g0 < ntag; g0 += kWave) {
-    // ---- this group's tags, one a lane (valid: the walk checked them).
-    const bool on = g0 + lane < ntag;
-    const uint32_t pos = on ? (uint32_t)tp[g0 + lane] : 0u;
-    const uint64_t tv = view8(src + pos);
-    const uint32_t tag = (uint32_t)tv & 0xffu, kind = tag & 3u, m0 = tag >> 2;
-    const uint32_t b1 = (uint32_t)(tv >> 8);
-    const uint32_t extra = m0 >= 60 ? m0 - 59 : 0u;              // snappy.c:216-256
-    const uint32_t emask = extra >= 4 ? 0xffffffffu : (1u << (8 * (extra & 3u))) - 1u;
-    const uint32_t lm = extra ? (b1 & emask) : m0;
-    const uint32_t clen = kind == 1 ? 4 + (m0 & 7u) : m0 + 1;    // snappy.c:276-317
-    const uint32_t dist = kind == 1 ? ((tag & 0xe0u) << 3) | (b1 & 0xffu)
-                                    : (kind == 2 ? b1 & 0xffffu : b1);
-    const bool lit = on & (kind == 0);
-    const bool cp = on & (kind != 0);
-    const uint32_t len = !on ? 0u : (kind == 0 ? lm + 1 : clen);
-    const uint32_t incl = wave_incl_sum(len);
-    const uint32_t at = made + incl - len;                       // the op's output offset
-    const uint32_t total = lane_val(incl, kWave - 1);
-
-    // ---- literals: 16 bytes a lane per step, four steps' loads in flight.
-    {
-      const gptr<const uint8_t> ls = src + (pos + 1 + extra);
-      const uint32_t full = lit ? (len & ~15u) : 0u;
-#pragma clang loop unroll(disable)
-      for (uint32_t c = 0; ballot(c < full); c += 64) {
-        u32x4 v[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t q = c + 16 * k;
-          v[k] = ld16(ls + (q < full ? q : 0u));
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t q = c + 16 * k;
-          if (q < full) lwr16(o + at + q, v[k]);
-        }
-      }
-      const uint32_t r = lit ? (len & 15u) : 0u;
-      if (ballot(r != 0)) {
-        const u32x4 v = ld16(ls + full);
-        lds_put_head(o + at + full, v, r);
-      }
-    }
-    order();
-    const uint64_t cps = ballot(cp);
-    if (cps) {
-      // ---- which copies read a byte another copy of this group writes:
-      // mark every copy's output, test every copy's source (a source lies
-      // wholly before its own output unless it overlaps itself, dist < len).
-      const Span3 d = span3(cp ? at : 0u, cp ? len : 0u);
-      if (cp) {
-        __hip_atomic_fetch_or(&s_mark[d.w], d.m0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(&s_mark[d.w + 1], d.m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(&s_mark[d.w + 2], d.m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      order();
-      const uint32_t sa = cp ? at - dist : 0u;
-      const Span3 q = span3(sa, cp ? len : 0u);
-      const uint32_t hit = (s_mark[q.w] & q.m0) | (s_mark[q.w + 1] & q.m1) | (s_mark[q.w + 2] & q.m2);
-      order();
-      if (cp) {
-        s_mark[d.w] = 0;
-        s_mark[d.w + 1] = 0;
-        s_mark[d.w + 2] = 0;
-      }
-      const bool seq = cp & ((hit != 0) | (dist < len));
-      // ---- copies that read no byte of this group's copies: all at once
-      // (each reads only bytes already final: literals placed above, earlier
-      // groups), 16 bytes a lane per step.
-      const bool par = cp & !seq;
-      if (ballot(par)) {
-        const uint32_t full = par ? (len & ~15u) : 0u;
-        u32x4 v[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) v[k] = lrd16(o + (par ? sa + 16 * k : 0u));
-        order();
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-          if (16 * k < full) lwr16(o + at + 16 * k, v[k]);
-        const uint32_t r = par ? (len & 15u) : 0u;
-        const uint32_t kr = full >> 4;
-        const u32x4 vt = kr == 0 ? v[0] : (kr == 1 ? v[1] : (kr == 2 ? v[2] : v[3]));
-        if (r) lds_put_head(o + at + full, vt, r);
-        order();
-      }
-      // ---- the others in stream order, 64 lanes a copy (snappy.c:326-331:
-      // an overlapping copy repeats its dist-byte pattern).
-#pragma clang loop unroll(disable)
-      for (uint64_t sm = ballot(seq); sm; sm &= sm - 1) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(sm);
-        const uint32_t A = lane_val(at, l), D = lane_val(dist, l), L = lane_val(len, l);
-        uint32_t r = lane;
-        if (D < L) {
-          const float rd = __builtin_amdgcn_rcpf((float)D);
-          const uint32_t qq = (uint32_t)((float)lane * rd);
-          r = lane - qq * D;
-          if ((int32_t)r < 0) r += D;
-          if (r >= D) r -= D;
-        }
-        const uint8_t b = o[A - D + r];
-        if (lane < L) o[A + lane] = b;
-        order();
-      }
-    }
-    made += total;
-  }
-  order();
-  flush_out(dst, s_img, want);
-}
-
-hipError_t launch_decode_twopass(const DecodeArgs& a, hipStream_t s) {
-  using namespace twopass;
-  if (a.one.on) return hipErrorInvalidValue;
-  const size_t tp_bytes = ((size_t)a.n * kTagCap * sizeof(uint16_t) + 255) & ~(size_t)255;
-  Scratch scratch(tp_bytes + (size_t)a.n * sizeof(uint32_t) + 256, s);
-  if (scratch.status() != hipSuccess) return scratch.status();
-  uint16_t* tp = (uint16_t*)scratch.get();
-  uint32_t* meta = (uint32_t*)((uint8_t*)scratch.get() + tp_bytes);
-  hipLaunchKernelGGL(decode_walk_kernel, dim3((a.n + kWave - 1) / kWave), dim3(kWave), 0, s, a.in,
-                     a.in_off, a.in_len, a.out_cap, a.out_len, a.status, a.index, a.n, a.count,
-                     tp, meta);
-  hipLaunchKernelGGL(decode_place_kernel, dim3(a.n), dim3(kWave), 0, s, a.in, a.in_off, a.in_len,
-                     a.out, a.out_off, a.out_len, a.status, a.index, a.n, a.count, tp, meta);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return scratch.release();
-}
-#endif  // LGS_PROBE_DECODERS
 
 
 
@@ -1505,11 +1186,6 @@ static hipError_t launch_decode_split(const DecodeArgs& a, uint32_t max_out, hip
     LGS_TRY(launch_decode_ops(c, s));
   } else
 #endif
-#ifdef LGS_PROBE_DECODERS
-  if (force == kDecTwoPass) {
-    LGS_TRY(launch_decode_twopass(c, s));
-  } else
-#endif
   LGS_TRY((a.n >= kLaneMinBlocks || force == kDecRing ? launch_decode_ring(c, s)
                                                       : launch_decode_cls<kDecCap0, 1>(c, s)));
   c.index = list + a.n; c.count = cnt + 1;
@@ -1534,13 +1210,10 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t max_out, hipStream_t s) {
   if (force == kDecOps && max_out <= kDecCap0) return launch_decode_ops(a, s);
   if (force == kDecQuad) return launch_decode_quad(a, s);
 #endif
-  if ((force == kDecAuto || force == kDecOps || force == kDecTwoPass || force == kDecRing) &&
+  if ((force == kDecAuto || force == kDecOps || force == kDecRing) &&
       !a.index && max_out > kDecCap0 && a.n >= kSplitMinBlocks &&
       options().split.load(std::memory_order_relaxed))
     return launch_decode_split(a, max_out, s);
-#ifdef LGS_PROBE_DECODERS
-  if (force == kDecTwoPass && max_out <= kDecCap0 && !a.one.on) return launch_decode_twopass(a, s);
-#endif
   if (force == kDecRing || (force == kDecAuto && a.n >= kLaneMinBlocks))
     return launch_decode_ring(a, s);
 #ifdef LGS_PROBE_DECODERS

@@ -15,8 +15,7 @@ namespace lgs {
 // LGS_DECODE_KERNEL / LGS_NO_SPLIT, read once at load -- nothing on the
 // launch path reads the environment).
 enum DecodeKernel {
-  kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4, kDecGroup = 5, kDecChain = 6,
-  kDecTwoPass = 7
+  kDecAuto = 0, kDecRing = 1, kDecWave = 2, kDecQuad = 3, kDecOps = 4, kDecGroup = 5, kDecChain = 6
 };
 // Outputs over the 16 KiB class: the one-tag walk (default), or, in the
 // probe library, the trip decoder or the workgroup decoder.
@@ -65,13 +64,9 @@ hipError_t launch_decode_quad(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_ops(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_trips(const DecodeArgs& a, hipStream_t s);
 #endif
-// The ring decoder (lane per block), for the split launch and A/Bs.
+// The ring decoder (lane per block, large batches), for the split launch.
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
-#ifdef LGS_PROBE_DECODERS
-// Probe library only: the two-pass decoder (walk kernel + place kernel,
-// outputs <= 4 608 bytes).
-hipError_t launch_decode_twopass(const DecodeArgs& a, hipStream_t s);
-#endif
+
 #ifdef LGS_PROBE_DECODERS
 // Probe library only: the workgroup (pointer-jumping) decoder of
 // lgs_decode_group.hip, outputs up to kGroupMaxOut bytes, and the chain

@@ -208,7 +208,7 @@ def test_random_inputs_vs_oracle(gpu):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops", "group", "chain", "twopass"]))
+@pytest.mark.parametrize("kernel", _with_probe(["wave", "ring"], ["quad", "ops", "group", "chain"]))
 def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
     # Every decode kernel (forced through lgs_set_option) against the
     # reference's accept/reject bit and output, on every golden stream.
@@ -227,7 +227,7 @@ def test_decode_kernel_variants_golden(gpu, vectors, kernel, force):
             assert s in (gpu.LGS_ST_CORRUPT, gpu.LGS_ST_NOSPACE), (kernel, v.name)
 
 
-@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops", "group", "chain", "twopass")]))
+@pytest.mark.parametrize("kernels", _with_probe([("ring", "wave")], [("quad", "ops", "group", "chain")]))
 def test_decode_kernels_c2_full_size(gpu, digests, force, kernels):
     import torch
     from lcdb_amd import batch
@@ -426,7 +426,7 @@ def test_encode_c2_and_random(gpu, digests):
         assert o == ref.encode(b)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops", "group", "twopass"]))
+@pytest.mark.parametrize("kernel", _with_probe(["ring"], ["quad", "ops", "group"]))
 def test_decode_ring_c3_mixed_and_odd_slots(gpu, digests, force, kernel):
     # The LDS-ring decoder on C3 (4/16/64 KiB classes, half random: long
     # literals streamed through the input window, far copies) and on output
@@ -559,7 +559,7 @@ if PROBE:   # the two-pass decoder exists in the probe library only
 
 
 
-@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops", "group", "chain", "twopass"]))
+@pytest.mark.parametrize("kernel", _with_probe([None, "ring"], ["quad", "ops", "group", "chain"]))
 def test_decode_in_place_runahead(gpu, kernel, force):
     # One batch per output size, so each LDS class of the wave decoder (4, 16
     # and 64 KiB, chosen by the largest capacity) is the one that runs.
@@ -929,15 +929,15 @@ def _op_stream(rng, want_max=4608, max_ops=None):
     return _varint(len(out)) + bytes(body), bytes(out)
 
 
-@pytest.mark.parametrize("kernel", _with_probe(["auto", "wave"], ["twopass"]))
+@pytest.mark.parametrize("kernel", _with_probe(["auto", "wave"], ["ops"]))
 def test_op_streams(gpu, force, kernel):
     # Streams built op by op: every tag form, overlapping copies (dist < len),
     # chains of copies of copies, streams of many tiny ops, and their
     # truncations and corruptions -- against the reference's decode.  "auto"
     # repeats them past the ring decoder's threshold (36 864 blocks); "wave"
-    # forces the wave decoder; the probe library's two-pass decoder
-    #  takes the same streams, including more tags than its walk
-    # records (its slow path).
+    # forces the wave decoder; the probe library's two-pass decoder ("ops",
+    # DESIGN 4.2) takes the same streams, including more ops than its first
+    # pass records (its slow path).
     import random
     force("decoder", kernel)
     rng = random.Random(606)

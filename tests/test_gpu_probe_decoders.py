@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # Every probe case test_gpu_parity.py defines (its parametrizations over the
-# quad, ops, group, chain, trips and two-pass decoders): the child must pass exactly these,
+# quad, ops, group, chain, trips decoders): the child must pass exactly these,
 # so a case that silently stops being collected fails here.
 EXPECTED = {
     "test_decode_kernel_variants_golden[quad]", "test_decode_kernel_variants_golden[ops]",
@@ -42,8 +42,7 @@ EXPECTED = {
     "test_decode_small_batch_kernels_and_rejects[group-66048]",
     "test_decode_small_batch_kernels_and_rejects[chain-4608]",
     "test_decode_small_batch_kernels_and_rejects[chain-16896]",
-    "test_decode_kernel_variants_golden[twopass]", "test_decode_ring_c3_mixed_and_odd_slots[twopass]",
-    "test_decode_in_place_runahead[twopass]", "test_op_streams[twopass]",
+    "test_op_streams[ops]",
 }
 
 
