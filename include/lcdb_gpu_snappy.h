@@ -325,7 +325,10 @@ int lgs_service_resume(void);
      "decoder": "auto" | "ring" (lane-per-block) | "wave" (wave-per-block)
      "wide":    "walk"  (decoder of outputs over 16 KiB: the one-tag walk)
      "split":   "1" | "0"  (size-class split of mixed batches, see above)
-   Initial values: LGS_DECODE_KERNEL, LGS_NO_SPLIT=1, read once at load.
+     "service": "1" | "0"  (the drop-in's resident waves)
+     "verify_overlap": "1" | "0"  (table reads: CRC pass beside the decoder)
+   Initial values: LGS_DECODE_KERNEL, LGS_NO_SPLIT=1, LGS_DROPIN_SERVICE,
+   LGS_VERIFY_OVERLAP=0, read once at load.
    LGS_EINVAL for an unknown name or value.  (The decoders that lost their
    A/B -- "decoder" "quad", "ops", "group" and "chain", "wide" "trips" and
    "group" --

@@ -30,7 +30,7 @@ PROBE_SOURCES = ["lgs_decode_probe.hip", "lgs_decode_group.hip", "lgs_decode_cha
 HIP_SOURCES = ["lgs_api.cpp", "lgs_encode_service.hip", "lgs_decode.hip",
                "lgs_table.hip", "lgs_bloom.hip", "lgs_table_index.cpp", "lgs_probe.hip"]
 HIP_HEADERS = ["lgs_device.h", "lgs_launch.h", "lgs_decode_common.h", "lgs_probe_hooks.h",
-               "lgs_service.h"]
+               "lgs_service.h", "lgs_crc.h"]
 # Only ldb_snappy_* and lgs_* are exported (the library is loaded into lcdb).
 EXPORTS_MAP = os.path.join(CSRC, "exports.map")
 # The files that define the two profiled codec kernels and how they are

@@ -166,6 +166,49 @@ def test_write_blocks_vs_oracle(tab, compression):
     assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
 
 
+def _small_blocks(n):
+    """n blocks of at most 4608 bytes (the fused write's range): fillseq
+    blocks, random and zero blocks of every awkward length, the 12.5 % edge."""
+    rng = random.Random(0x5a11)
+    from lcdb_amd import corpus
+    c = corpus.fillseq(max(n // 2, 1))
+    blocks = [c.block(i) for i in range(n // 2)]
+    while len(blocks) < n:
+        k = rng.randrange(6)
+        if k == 0:
+            blocks.append(rng.randbytes(rng.choice([0, 1, 2, 3, 4, 5, 16, 17, 63, 64, 65, 4608])))
+        elif k == 1:
+            blocks.append(bytes(rng.randrange(4609)))
+        elif k == 2:
+            half = rng.randbytes(rng.randrange(8, 3800))
+            pad = len(half) // 6 + rng.randrange(-3, 4)
+            blocks.append(half + bytes(max(pad, 0)))
+        else:
+            blocks.append(c.block(rng.randrange(c.n))[:rng.randrange(4609)])
+    rng.shuffle(blocks)
+    return blocks
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 5000])
+def test_write_small_blocks_vs_oracle(tab, n):
+    # Blocks <= 4608 B (the one-stride encode slots), host and device entry.
+    import torch
+    blocks = _small_blocks(n)
+    assert max(len(b) for b in blocks) <= 4608
+    want = oracle.table_write_blocks(blocks, 1, 777)
+    got = tab.write_blocks_host(blocks, 1, 777)
+    assert got[3] == want[3]
+    assert got[0] == want[0]
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2])
+    buf, off, ln = _device_pack(blocks, torch, 3)
+    d_file, hoff, hsize, end = tab.write_blocks(buf, off, ln, 1, 777)
+    torch.cuda.synchronize()
+    assert int(end.cpu()[0]) == want[3]
+    assert d_file[:want[3] - 777].cpu().numpy().tobytes() == want[0]
+    assert np.array_equal(hoff.cpu().numpy().astype(np.uint64), want[1])
+    assert np.array_equal(hsize.cpu().numpy().astype(np.uint64), want[2])
+
+
 def test_write_blocks_device_fillseq(tab):
     import torch
     from lcdb_amd import corpus
