@@ -1062,6 +1062,9 @@ Options& options() { return options_init(); }
 // off[i] = i * stride (lgs_table.hip; declared here, not in lgs_launch.h,
 // whose text keys the codec kernels' traffic figures).
 hipError_t launch_fill_stride(uint64_t* off, uint64_t stride, uint32_t n, hipStream_t s);
+// check_kernel's checks with one lane per handle, no CRC (lgs_table.hip;
+// declared here for the same reason).
+hipError_t launch_check_lane(const CheckArgs& a, hipStream_t s);
 
 }  // namespace lgs
 
@@ -1479,7 +1482,9 @@ static int table_read(const uint8_t* d_file, uint64_t file_len, const uint64_t* 
   EventPair ev;
   CheckArgs c{d_file, file_len, d_hoff, d_hsize, verify && !a ? 1u : 0u, d_out, d_out_off, d_out_cap,
               d_out_len, d_status, dec_in_off, dec_len, dec_off, dec_cap, dummy_off, n};
-  LGS_HIP(launch_check(c, s));
+  // (Without verification: one lane per handle; ahead of the verify pass the
+  // wave-per-block check, lgs_table.hip.)
+  LGS_HIP(verify ? launch_check(c, s) : launch_check_lane(c, s));
   if (a) {
     // After the type dispatch: queued with it, both ran slower (profiles/r6j),
     // and queued first but sleeping through it, its workgroups took the CUs

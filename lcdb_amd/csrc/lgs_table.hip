@@ -10,22 +10,25 @@
 //    truncation check, the trailer CRC check (verify_checksums), the type
 //    dispatch, raw copy or snappy decode (lgs_decode.hip).
 //
-// CRC on half a wave (two blocks per wave, any length).  CRC32C is linear
-// over GF(2), so the 32 lanes of a half split a block into 80-byte
-// segments, one per lane, and combine them:
+// CRC32C on a wave (lgs_crc.h; one block per wave by default, two with
+// LGS_CRC_LANES=32).  CRC32C is linear over GF(2), so the lanes split a
+// block into segments of kSeg bytes (48 by default), one per lane, and
+// combine them:
 //  * the block's bytes are taken where they lie, as the aligned 16-byte
 //    granules that hold them (only those: never another page), extended by
 //    t < 16 trailing zeros to the end of the last granule and by leading
-//    zeros to a multiple of 2560 bytes (a "pass" = 32 lanes x 80 bytes).
+//    zeros to a whole number of passes (a "pass" = lanes x kSeg bytes).
 //    Leading zeros leave a register that is 0 at 0; the ~0
 //    pre-conditioning is the start register of the lane holding byte 0
 //    (the register that its leading zeros turn into ~0); the trailing
 //    zeros are divided out at the end (a multiplication by x^(-8t));
-//  * a lane folds its 20 dwords with slice-by-4 tables (4 LDS lookups per
-//    dword), then multiplies its CRC by x^(640 (31 - lane)) -- the zero
-//    bytes after its segment -- with a table of its own (eight nibble
-//    lookups), and one xor-reduction over the half (DPP) gives the pass's
-//    CRC.  The CRC of the passes before enters as lane 0's start register.
+//  * a lane folds its dwords with slice-by-8 tables (eight bytes per
+//    dependent step; slice-by-4 in the verify pass's small image), then
+//    multiplies its CRC by x^(8 kSeg (lanes - 1 - lane)) -- the zero bytes
+//    after its segment -- with a table of its own (eight nibble lookups),
+//    and one DPP xor-reduction gives the pass's CRC (the small image: a
+//    butterfly of shifts instead).  The CRC of the passes before enters as
+//    lane 0's start register.
 // Copies to the destination (the file image on the write path, the output
 // slot of a raw block on the read path) are a pass of their own over whole
 // aligned destination granules (copy_bytes).
@@ -199,7 +202,10 @@ constexpr uint8_t kPending = 0xff;   // snappy block: status decided by the deco
 // format.c:162-231, 263-267 per handle; snappy blocks (:233-261) are handed
 // to the decoder through dec_in_off/dec_len/dec_off/dec_cap (others get an
 // empty input at file offset 0 and a zero-capacity dummy slot, so the
-// decoder cannot touch their output).
+// decoder cannot touch their output).  CRC: the trailer checks here
+// (verify_checksums without the overlapped verify pass); without them this
+// instance runs ahead of the decoder and verify_kernel (table_read), and
+// check_lane_kernel below serves reads without verification.
 template <uint32_t WAVES, bool CRC>
 __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     const uint8_t* __restrict__ file, uint64_t file_len, const uint64_t* __restrict__ hoff,
@@ -209,8 +215,6 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
     uint64_t* __restrict__ dec_in_off, uint32_t* __restrict__ dec_len,
     uint64_t* __restrict__ dec_off, uint32_t* __restrict__ dec_cap, uint64_t dummy_off,
     uint32_t n) {
-  // Without CRC (verify == 0, or the checks run in verify_kernel) no tables:
-  // this instance holds no LDS and runs beside verify_kernel.
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[CRC ? kTabWords : 4];
   if (CRC) load_tables<64 * WAVES, kTabWords>(s_tab);
   const Crc T{{s_tab}};
@@ -271,6 +275,61 @@ __global__ __launch_bounds__(64 * WAVES) void check_kernel(
       dec_off[i] = snappy ? oo : dummy_off;
       dec_cap[i] = snappy ? cap : 0u;
     }
+  }
+}
+
+// check_kernel for reads without verify_checksums (lcdb's default): one lane
+// per handle -- the checks are a few loads and compares a block, and a wave
+// per block spent 15.8 us on C2's 65 536 handles -- then the wave copies its
+// raw blocks one after the other, every lane on each.  (Ahead of the
+// overlapped verify pass it loses: 350 against 331 us on C2's verified read,
+// profiles/r8e_check_lane_ab.txt -- the wave-per-block check's length is what
+// lets the decoder's workgroups take their CUs before verify_kernel's.)
+__global__ __launch_bounds__(256) void check_lane_kernel(
+    const uint8_t* __restrict__ file, uint64_t file_len, const uint64_t* __restrict__ hoff,
+    const uint64_t* __restrict__ hsize, uint8_t* __restrict__ out,
+    const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ out_cap,
+    uint32_t* __restrict__ out_len, uint8_t* __restrict__ status,
+    uint64_t* __restrict__ dec_in_off, uint32_t* __restrict__ dec_len,
+    uint64_t* __restrict__ dec_off, uint32_t* __restrict__ dec_cap, uint64_t dummy_off,
+    uint32_t n) {
+  const uint32_t lane = lane_id();
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (uni(blockIdx.x * 256 + (threadIdx.x & ~63u)) >= n) return;   // a whole wave past n
+  const bool on = i < n;
+  const uint64_t off = on ? hoff[i] : 0, size = on ? hsize[i] : 0;
+  const uint32_t cap = on ? out_cap[i] : 0u;
+  const uint64_t oo = on ? out_off[i] : 0;
+  // format.c:174-198, as check_kernel.
+  const bool bad_size = size > ~0ull - kTrailer;                      // :174-175
+  const bool io = !bad_size && (off > file_len || file_len - off < size + kTrailer);  // :195-198
+  const bool big = !bad_size && !io && size > 0x7fffffffull;          // beyond this ABI
+  const bool body = on && !bad_size && !io && !big;
+  const uint32_t sz = body ? (uint32_t)size : 0u;
+  const uint32_t ty = body ? (uint32_t)file[off + sz] : 0u;
+  const bool raw_fits = body && ty == 0 && sz <= cap;
+  uint32_t st = kStCorrupt, olen = 0;
+  if (bad_size) st = kStCorrupt;
+  else if (io) st = kStIoErr;
+  else if (big) st = kStNoSpace;
+  else if (ty == 0) { st = raw_fits ? kStOk : kStNoSpace; olen = raw_fits ? sz : 0u; }  // :213-231
+  else if (ty == 1) st = kPending;                                    // :233-261
+  else st = kStBadType;                                               // :263-267
+  const bool snappy = body && ty == 1;
+  if (on) {
+    status[i] = (uint8_t)st;
+    out_len[i] = olen;
+    dec_in_off[i] = snappy ? off : 0u;   // never an out-of-range address
+    dec_len[i] = snappy ? sz : 0u;
+    dec_off[i] = snappy ? oo : dummy_off;
+    dec_cap[i] = snappy ? cap : 0u;
+  }
+  // The raw blocks (format.c:213-231), a wave at a time.
+  for (uint64_t m = ballot(raw_fits); m; m &= m - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+    const uint64_t so = ((uint64_t)lane_val((uint32_t)(off >> 32), l) << 32) | lane_val((uint32_t)off, l);
+    const uint64_t d = ((uint64_t)lane_val((uint32_t)(oo >> 32), l) << 32) | lane_val((uint32_t)oo, l);
+    copy_block(to_global(file) + so, to_global(out) + d, lane_val(sz, l), lane);
   }
 }
 
@@ -462,6 +521,14 @@ hipError_t launch_check(const CheckArgs& a, hipStream_t s) {
                        a.out, a.out_off, a.out_cap, a.out_len, a.status, a.dec_in_off, a.dec_len,
                        a.dec_off, a.dec_cap, a.dummy_off, a.n);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_check_lane(const CheckArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(check_lane_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a.file,
+                     a.file_len, a.hoff, a.hsize, a.out, a.out_off, a.out_cap, a.out_len,
+                     a.status, a.dec_in_off, a.dec_len, a.dec_off, a.dec_cap, a.dummy_off, a.n);
   return hipGetLastError();
 }
 

@@ -21,6 +21,6 @@ for r in 1 2; do
     timeout -k 10 300 env $envv python tools/bench_table.py --iters 10 $arg > gpurun_out/${P}_bt_${tag}_$r.json 2>&1 || { tail -5 gpurun_out/${P}_bt_${tag}_$r.json; exit 1; }
     python -c "
 import json; d=json.loads([l for l in open('gpurun_out/${P}_bt_${tag}_$r.json') if l.startswith('{')][-1])
-print('$tag $r', {k: round(d[k]*1000,1) for k in ('write_ms','read_ms','crc_ms')}, d['parity'][:30])"
+print('$tag $r', {k: round(d[k]*1000,1) for k in ('write_ms','read_ms','read_noverify_ms','crc_ms') if k in d}, d['parity'][:30])"
   done
 done
