@@ -259,18 +259,19 @@ def test_read_blocks_corrupted_matches_reference(tab, ref_tables, tmp_path, veri
                 assert res[i] == dd.contents[i]
 
 
-@pytest.mark.parametrize("overlap", ["1", "0"])
-def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path, overlap, force):
+@pytest.mark.parametrize("verify,overlap", [(True, "1"), (True, "0"), (False, "1")])
+def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path, verify, overlap, force):
+    # verify False: the checks one lane per handle (check_lane_kernel).
     force("verify_overlap", overlap)
     path, file, d = ref_tables[256]
     n = len(file)
     handles = [(0, n), (n - 4, 0), (n - 5, 0), (n, 0), (n + 10, 3),
                (int(d.off[1]), int(d.size[1]) + 1), (int(d.off[2]) + 1, int(d.size[2])), (1, 2),
                (0, 0), (2**64 - 100, 50), (5, 2**64 - 3)]
-    dd = table_io.dump_blocks(path, str(tmp_path / "h.bin"), True, handles)
+    dd = table_io.dump_blocks(path, str(tmp_path / "h.bin"), verify, handles)
     off = np.array([h[0] for h in handles], dtype=np.uint64)
     size = np.array([h[1] for h in handles], dtype=np.uint64)
-    res, st = tab.read_blocks_host(file, off, size, [1 << 17] * len(handles), True)
+    res, st = tab.read_blocks_host(file, off, size, [1 << 17] * len(handles), verify)
     for i in range(len(handles)):
         assert table_io.same_outcome(int(st[i]), dd.rc[i]), (i, st[i], dd.rc[i])
         assert res[i] == (dd.contents[i] if dd.rc[i] == LDB_OK else None)
@@ -291,12 +292,12 @@ def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path, overlap, f
     sizes = np.array([len(b) for b in blocks], dtype=np.uint64)
     offs = np.array(offs, dtype=np.uint64)
     caps = [4096] * len(blocks)
-    res, st = tab.read_blocks_host(bytes(region), offs, sizes, caps, True)
+    res, st = tab.read_blocks_host(bytes(region), offs, sizes, caps, verify)
     for i in range(len(blocks)):
-        ost, ores = oracle.table_read_block(bytes(region), int(offs[i]), int(sizes[i]), True, caps[i])
+        ost, ores = oracle.table_read_block(bytes(region), int(offs[i]), int(sizes[i]), verify, caps[i])
         assert int(st[i]) == ost and res[i] == ores, i
-    assert list(st) == [tab.LGS_ST_BADTYPE, tab.LGS_ST_CORRUPT, tab.LGS_ST_NOSPACE] + \
-        [tab.LGS_ST_BADCRC] * 4
+    first = [tab.LGS_ST_BADTYPE, tab.LGS_ST_CORRUPT, tab.LGS_ST_NOSPACE]
+    assert list(st) == first + ([tab.LGS_ST_BADCRC] * 4 if verify else [tab.LGS_ST_OK] + first)
 
 
 @pytest.mark.parametrize("bs", [4096, 256, 65536])
