@@ -280,9 +280,9 @@ def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path, verify, ov
     # A wrong trailer CRC wins over every later outcome (format.c:203-211):
     # raw, bad type, snappy, too small a slot.
     blocks = [b"x" * 300, b"\x05hello", b"y" * 5000, b"z" * 100, b"w" * 50, b"\x05hello",
-              b"v" * 5000]
-    types = [2, 1, 0, 0, 2, 1, 0]
-    wrong = [0, 0, 0, 1, 1, 1, 1]
+              b"v" * 5000, bytes(range(40)), b"u" * 4096]
+    types = [2, 1, 0, 0, 2, 1, 0, 0, 0]
+    wrong = [0, 0, 0, 1, 1, 1, 1, 0, 0]
     region = bytearray()
     offs = []
     for b, ty, bad in zip(blocks, types, wrong):
@@ -297,7 +297,8 @@ def test_read_blocks_bad_handles_and_types(tab, ref_tables, tmp_path, verify, ov
         ost, ores = oracle.table_read_block(bytes(region), int(offs[i]), int(sizes[i]), verify, caps[i])
         assert int(st[i]) == ost and res[i] == ores, i
     first = [tab.LGS_ST_BADTYPE, tab.LGS_ST_CORRUPT, tab.LGS_ST_NOSPACE]
-    assert list(st) == first + ([tab.LGS_ST_BADCRC] * 4 if verify else [tab.LGS_ST_OK] + first)
+    assert list(st) == first + ([tab.LGS_ST_BADCRC] * 4 if verify else [tab.LGS_ST_OK] + first) + \
+        [tab.LGS_ST_OK] * 2                       # raw blocks of 40 and 4 096 bytes
 
 
 @pytest.mark.parametrize("bs", [4096, 256, 65536])
